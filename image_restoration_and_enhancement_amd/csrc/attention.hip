@@ -1,0 +1,273 @@
+// irx — flash-style multi-head attention for gfx950 (wave64, MFMA 16x16).
+//
+// Serves the UNet's self-attention (attn1: Lq = Lk = h*w up to 9216, d = 40/80/160),
+// cross-attention (attn2: Lk = 77 text tokens) and CLIP's causal self-attention (d = 64).
+// "Swapped" formulation: each wave computes S^T = K Q^T so a lane owns one query COLUMN;
+// its softmax statistics are lane-local (plus a 4-way shuffle for the max), the
+// exponentiated tile is already the B operand of O^T = V^T P^T (no LDS round trip for P),
+// and V^T fragments come straight out of the row-major V tile through the gfx950
+// transposing LDS read ds_read_b64_tr_b16.  Online softmax in fp32; scores never touch HBM.
+// bf16: v_mfma_f32_16x16x16_bf16 (K = 16 keeps d = 40 / 80 padding at 48 / 80);
+// fp32 (parity mode): exact-f32 v_mfma_f32_16x16x4_f32.
+#include "ops.h"
+
+namespace irx {
+namespace {
+
+constexpr int kWaves = 4;
+constexpr int kQT = 2;               // 16-query column tiles per wave
+constexpr int kQB = kWaves * kQT * 16;  // queries per block (128)
+constexpr int kKT = 64;              // keys per LDS tile
+
+template <typename T, int DP>
+struct AttnLds {
+  // K tile rows: stride chosen so 16 rows x 2 half-chunks of ds_read_b64 are bank-disjoint;
+  // V tile rows: stride chosen so the transposed reads (8 rows x 4 chunks per half wave) are.
+  static constexpr int SK = sizeof(T) == 2 ? DP + 8 : DP + 4;
+  static constexpr int SV = sizeof(T) == 2 ? (((DP / 2) % 16 == 8) ? DP : DP + 16) : DP + 1;
+};
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+template <typename T, int DP>
+__global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
+  using L = AttnLds<T, DP>;
+  constexpr int ND = DP / 16;
+  constexpr int SK = L::SK, SV = L::SV;
+  __shared__ __attribute__((aligned(16))) T Ks[kKT * SK];
+  __shared__ __attribute__((aligned(16))) T Vs[kKT * SV];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int qb0 = blockIdx.x * kQB;
+  const int q0 = qb0 + wave * (kQT * 16);
+  const int d = a.d;
+
+  const T* __restrict__ Q = (const T*)a.q + (long)b * a.sq + (long)h * d;
+  const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * d;
+  const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * d;
+
+  // zero the padded LDS columns once (loads only ever write columns < d)
+  for (int i = tid; i < kKT * SK; i += 256) Ks[i] = T(0);
+  for (int i = tid; i < kKT * SV; i += 256) Vs[i] = T(0);
+
+  // ---- Q^T fragments in registers (B operand: k = d, col = query)
+  constexpr int QV = sizeof(T) == 2 ? 1 : 4;       // f32: float4 per lane per 16-deep chunk
+  typedef typename std::conditional<sizeof(T) == 2, s16x4, f32x4>::type qfrag_t;
+  qfrag_t qf[kQT][ND];
+#pragma unroll
+  for (int qt = 0; qt < kQT; ++qt) {
+    const int q = q0 + qt * 16 + li;
+#pragma unroll
+    for (int dc = 0; dc < ND; ++dc) {
+      const int e = dc * 16 + 4 * g;
+      if constexpr (sizeof(T) == 2) {
+        s16x4 v = {0, 0, 0, 0};
+        if (q < a.Lq && e < d) v = *(const s16x4*)(Q + (long)q * a.ldq + e);
+        qf[qt][dc] = v;
+      } else {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (q < a.Lq && e < d) v = *(const f32x4*)(Q + (long)q * a.ldq + e);
+        qf[qt][dc] = v;
+      }
+    }
+  }
+  (void)QV;
+
+  f32x4 o[ND][kQT];
+#pragma unroll
+  for (int i = 0; i < ND; ++i)
+#pragma unroll
+    for (int j = 0; j < kQT; ++j) o[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrow[kQT], lrow[kQT];
+#pragma unroll
+  for (int j = 0; j < kQT; ++j) { mrow[j] = -INFINITY; lrow[j] = 0.f; }
+
+  const float sl2 = a.scale * 1.4426950408889634f;
+  int kend = a.Lk;
+  if (a.causal) kend = min(kend, qb0 + kQB);
+  const int cpr = d * (int)sizeof(T) / 16;           // 16-byte chunks per K/V row
+
+  for (int j0 = 0; j0 < kend; j0 += kKT) {
+    __syncthreads();   // previous tile fully consumed
+    for (int idx = tid; idx < kKT * cpr; idx += 256) {
+      const int r = idx / cpr, c = idx - r * cpr;
+      const int key = j0 + r;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (key < a.Lk) {
+        kv = *(const uint4*)(K + (long)key * a.ldk + c * (16 / (int)sizeof(T)));
+        vv = *(const uint4*)(V + (long)key * a.ldv + c * (16 / (int)sizeof(T)));
+      }
+      constexpr int E = 16 / (int)sizeof(T);
+      if constexpr (sizeof(T) == 2) {
+        *(uint4*)(Ks + r * SK + c * E) = kv;       // SK*2 bytes is a multiple of 16
+        if constexpr ((SV * 2) % 16 == 0) {
+          *(uint4*)(Vs + r * SV + c * E) = vv;
+        } else {
+          uint2* p = (uint2*)(Vs + r * SV + c * E);
+          p[0] = make_uint2(vv.x, vv.y); p[1] = make_uint2(vv.z, vv.w);
+        }
+      } else {
+        *(uint4*)(Ks + r * SK + c * E) = kv;
+        float* pv = (float*)(Vs + r * SV + c * E);
+        pv[0] = __uint_as_float(vv.x); pv[1] = __uint_as_float(vv.y);
+        pv[2] = __uint_as_float(vv.z); pv[3] = __uint_as_float(vv.w);
+      }
+    }
+    __syncthreads();
+
+    // ---- S^T = K Q^T  (rows = keys of this tile, cols = this wave's queries)
+    f32x4 s[4][kQT];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < kQT; ++qt) s[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int dc = 0; dc < ND; ++dc) {
+        const T* kp = Ks + (kt * 16 + li) * SK + dc * 16 + 4 * g;
+        if constexpr (sizeof(T) == 2) {
+          const s16x4 kf = *(const s16x4*)kp;
+#pragma unroll
+          for (int qt = 0; qt < kQT; ++qt)
+            s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[qt][dc], s[kt][qt], 0, 0, 0);
+        } else {
+          const f32x4 kf = *(const f32x4*)kp;
+#pragma unroll
+          for (int qt = 0; qt < kQT; ++qt) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[e], qf[qt][dc][e], s[kt][qt], 0, 0, 0);
+          }
+        }
+      }
+    }
+
+    // ---- online softmax per query column
+    typedef typename std::conditional<sizeof(T) == 2, s16x4, f32x4>::type pfrag_t;
+    pfrag_t pf[4][kQT];
+#pragma unroll
+    for (int qt = 0; qt < kQT; ++qt) {
+      const int q = q0 + qt * 16 + li;
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = j0 + kt * 16 + 4 * g + i;
+          float x = s[kt][qt][i] * sl2;
+          if (key >= a.Lk || (a.causal && key > q)) x = -INFINITY;
+          s[kt][qt][i] = x;
+          tmax = fmaxf(tmax, x);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      const float mnew = fmaxf(mrow[qt], tmax);
+      const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(mrow[qt] - mnew);
+      mrow[qt] = mnew;
+      float lsum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        float p[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          p[i] = (mnew == -INFINITY) ? 0.f : exp2f(s[kt][qt][i] - mnew);
+          lsum += p[i];
+        }
+        if constexpr (sizeof(T) == 2) {
+          s16x4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = (short)f2bf(p[i]);
+          pf[kt][qt] = v;
+        } else {
+          pf[kt][qt] = f32x4{p[0], p[1], p[2], p[3]};
+        }
+      }
+      lrow[qt] = lrow[qt] * alpha + lsum;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) o[dt][qt] *= alpha;
+    }
+
+    // ---- O^T += V^T P^T
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        if constexpr (sizeof(T) == 2) {
+          // 16-lane group g reads V rows 16kt+4g .. +3, cols 16dt .. +15, transposed:
+          // lane li gets column 16dt+li of those 4 rows = A[row d][k = 4g + j]
+          const T* vp = Vs + (kt * 16 + 4 * g + (li >> 2)) * SV + dt * 16 + 4 * (li & 3);
+          const s16x4 vf = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)vp);
+#pragma unroll
+          for (int qt = 0; qt < kQT; ++qt)
+            o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf, pf[kt][qt], o[dt][qt], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float vf = Vs[(kt * 16 + 4 * g + e) * SV + dt * 16 + li];
+#pragma unroll
+            for (int qt = 0; qt < kQT; ++qt)
+              o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, pf[kt][qt][e], o[dt][qt], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+
+  // ---- normalise and store O[q][h*d + e]
+  T* __restrict__ O = (T*)a.o + (long)b * a.so + (long)h * d;
+#pragma unroll
+  for (int qt = 0; qt < kQT; ++qt) {
+    float l = lrow[qt];
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int q = q0 + qt * 16 + li;
+    if (q >= a.Lq) continue;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const int e = dt * 16 + 4 * g;
+      if (e >= d) continue;
+      T* op = O + (long)q * a.ldo + e;
+      if constexpr (sizeof(T) == 2) {
+        s16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = (short)f2bf(o[dt][qt][i] * inv);
+        *(s16x4*)op = v;
+      } else {
+        *(f32x4*)op = o[dt][qt] * inv;
+      }
+    }
+  }
+}
+
+template <typename T>
+void launch_t(const AttnArgs& a, hipStream_t s) {
+  dim3 grid((a.Lq + kQB - 1) / kQB, a.H, a.B), block(256);
+  const int dp = (a.d + 15) / 16 * 16;
+  switch (dp) {
+    case 48: attn_kernel<T, 48><<<grid, block, 0, s>>>(a); break;
+    case 64: attn_kernel<T, 64><<<grid, block, 0, s>>>(a); break;
+    case 80: attn_kernel<T, 80><<<grid, block, 0, s>>>(a); break;
+    case 160: attn_kernel<T, 160><<<grid, block, 0, s>>>(a); break;
+    default: throw Error("attention: unsupported head dim " + std::to_string(a.d));
+  }
+  IRX_LAUNCH_CHECK();
+}
+
+}  // namespace
+
+void attention(const AttnArgs& a, hipStream_t s) {
+  const int es = a.dtype == F32 ? 4 : 2;
+  IRX_CHECK(a.B > 0 && a.H > 0 && a.Lq > 0 && a.Lk > 0 && a.d > 0, "empty attention");
+  IRX_CHECK(a.d % 4 == 0 && (a.d * es) % 16 == 0, "head dim must be a multiple of 16 bytes");
+  IRX_CHECK((a.ldk * es) % 16 == 0 && (a.ldv * es) % 16 == 0, "K/V rows must be 16-byte aligned");
+  IRX_CHECK((a.ldq * es) % 8 == 0 && (a.ldo * es) % 8 == 0, "Q/O rows must be 8-byte aligned");
+  IRX_CHECK(((uintptr_t)a.k % 16) == 0 && ((uintptr_t)a.v % 16) == 0, "K/V base alignment");
+  if (a.dtype == F32) launch_t<float>(a, s);
+  else launch_t<bf16_t>(a, s);
+}
+
+}  // namespace irx

@@ -1,0 +1,320 @@
+// irx — extern "C" boundary (include/irx.h).  Every entry point catches C++ exceptions and turns
+// them into a non-zero status plus a thread-local message, so the Python layer can log and fall
+// back the way src/inference.py does around its diffusers calls.
+#include <cstring>
+#include <string>
+
+#include "../../include/irx.h"
+#include "models.h"
+
+namespace irx {
+static thread_local std::string g_err;
+void set_error(const std::string& m) { g_err = m; }
+const char* last_error() { return g_err.c_str(); }
+}  // namespace irx
+
+using namespace irx;
+
+struct irx_model {
+  std::unique_ptr<Model> m;
+};
+
+#define IRX_API_BEGIN try {
+#define IRX_API_END                                       \
+  return 0;                                               \
+  }                                                       \
+  catch (const std::exception& e) {                       \
+    set_error(e.what());                                  \
+    return -1;                                            \
+  }                                                       \
+  catch (...) {                                           \
+    set_error("unknown error");                           \
+    return -1;                                            \
+  }
+
+static hipStream_t S(void* s) { return (hipStream_t)s; }
+
+template <typename X>
+static X* as(irx_model* h, int kind) {
+  IRX_CHECK(h && h->m, "null model");
+  IRX_CHECK(h->m->kind() == kind, "wrong model kind");
+  return static_cast<X*>(h->m.get());
+}
+template <typename X>
+static const X* as(const irx_model* h, int kind) {
+  IRX_CHECK(h && h->m, "null model");
+  IRX_CHECK(h->m->kind() == kind, "wrong model kind");
+  return static_cast<const X*>(h->m.get());
+}
+
+extern "C" {
+
+const char* irx_last_error(void) { return last_error(); }
+int irx_version(void) { return 1; }
+
+int irx_model_create(int kind, const irx_model_config* cfg, int dtype, irx_model** out) {
+  IRX_API_BEGIN
+  IRX_CHECK(cfg && out, "null argument");
+  IRX_CHECK(dtype == IRX_F32 || dtype == IRX_BF16, "dtype must be IRX_F32 or IRX_BF16");
+  auto* h = new irx_model;
+  try {
+    if (kind == IRX_MODEL_UNET) h->m.reset(new Unet(*cfg, dtype));
+    else if (kind == IRX_MODEL_VAE) h->m.reset(new Vae(*cfg, dtype));
+    else if (kind == IRX_MODEL_CLIP) h->m.reset(new Clip(*cfg, dtype));
+    else throw Error("unknown model kind");
+  } catch (...) {
+    delete h;
+    throw;
+  }
+  *out = h;
+  IRX_API_END
+}
+
+int irx_model_destroy(irx_model* m) {
+  IRX_API_BEGIN
+  delete m;
+  IRX_API_END
+}
+
+int irx_model_num_params(const irx_model* m, int* n) {
+  IRX_API_BEGIN
+  IRX_CHECK(m && n, "null argument");
+  *n = (int)m->m->manifest().size();
+  IRX_API_END
+}
+
+int irx_model_param_info(const irx_model* m, int i, irx_param_info* info) {
+  IRX_API_BEGIN
+  IRX_CHECK(m && info, "null argument");
+  const auto& man = m->m->manifest();
+  IRX_CHECK(i >= 0 && i < (int)man.size(), "param index out of range");
+  const ParamEntry& e = man[i];
+  info->name = e.name.c_str();
+  info->layout = e.layout;
+  info->dtype = e.dtype;
+  info->ndim = (int)e.shape.size();
+  for (int k = 0; k < 4; ++k) info->shape[k] = k < info->ndim ? e.shape[k] : 1;
+  info->offset = e.off;
+  info->bytes = e.bytes;
+  IRX_API_END
+}
+
+int irx_model_blob_bytes(const irx_model* m, size_t* bytes) {
+  IRX_API_BEGIN
+  IRX_CHECK(m && bytes, "null argument");
+  *bytes = m->m->blob_bytes();
+  IRX_API_END
+}
+
+int irx_model_bind(irx_model* m, void* blob, size_t bytes) {
+  IRX_API_BEGIN
+  IRX_CHECK(m, "null model");
+  m->m->bind(blob, bytes);
+  IRX_API_END
+}
+
+// ------------------------------------------------------------------ UNet
+int irx_unet_workspace_bytes(const irx_model* m, int B, int h, int w, size_t* bytes) {
+  IRX_API_BEGIN
+  IRX_CHECK(bytes && B > 0 && h > 0 && w > 0, "bad arguments");
+  *bytes = const_cast<Unet*>(as<Unet>(m, IRX_MODEL_UNET))->workspace_bytes(B, h, w);
+  IRX_API_END
+}
+int irx_unet_context_bytes(const irx_model* m, int B, int L, size_t* bytes) {
+  IRX_API_BEGIN
+  IRX_CHECK(bytes && B > 0 && L > 0, "bad arguments");
+  *bytes = as<Unet>(m, IRX_MODEL_UNET)->context_bytes(B, L);
+  IRX_API_END
+}
+int irx_unet_prepare_context(irx_model* m, void* s, const void* ctx, int B, int L, void* kv, void* ws, size_t cap) {
+  IRX_API_BEGIN
+  IRX_CHECK(ctx && kv, "null buffer");
+  as<Unet>(m, IRX_MODEL_UNET)->prepare_context(S(s), ctx, B, L, kv, (char*)ws, cap);
+  IRX_API_END
+}
+int irx_unet_forward(irx_model* m, void* s, const void* x, int B, int h, int w, const float* t, const void* kv, int L,
+                     float* eps, void* ws, size_t cap) {
+  IRX_API_BEGIN
+  IRX_CHECK(x && t && kv && eps && ws, "null buffer");
+  as<Unet>(m, IRX_MODEL_UNET)->forward(S(s), x, B, h, w, t, kv, L, eps, (char*)ws, cap);
+  IRX_API_END
+}
+int irx_unet_input_channels(const irx_model* m, int* c) {
+  IRX_API_BEGIN
+  IRX_CHECK(c, "null argument");
+  *c = as<Unet>(m, IRX_MODEL_UNET)->cin_pad();
+  IRX_API_END
+}
+
+// ------------------------------------------------------------------ VAE
+int irx_vae_encode_workspace_bytes(const irx_model* m, int B, int H, int W, size_t* bytes) {
+  IRX_API_BEGIN
+  IRX_CHECK(bytes && B > 0 && H > 0 && W > 0, "bad arguments");
+  *bytes = const_cast<Vae*>(as<Vae>(m, IRX_MODEL_VAE))->encode_ws(B, H, W);
+  IRX_API_END
+}
+int irx_vae_encode(irx_model* m, void* s, const void* img, int B, int H, int W, void* mom, void* ws, size_t cap) {
+  IRX_API_BEGIN
+  IRX_CHECK(img && mom && ws, "null buffer");
+  as<Vae>(m, IRX_MODEL_VAE)->encode(S(s), img, B, H, W, mom, (char*)ws, cap);
+  IRX_API_END
+}
+int irx_vae_decode_workspace_bytes(const irx_model* m, int B, int h, int w, size_t* bytes) {
+  IRX_API_BEGIN
+  IRX_CHECK(bytes && B > 0 && h > 0 && w > 0, "bad arguments");
+  *bytes = const_cast<Vae*>(as<Vae>(m, IRX_MODEL_VAE))->decode_ws(B, h, w);
+  IRX_API_END
+}
+int irx_vae_decode(irx_model* m, void* s, const void* z, int B, int h, int w, void* out, void* ws, size_t cap) {
+  IRX_API_BEGIN
+  IRX_CHECK(z && out && ws, "null buffer");
+  as<Vae>(m, IRX_MODEL_VAE)->decode(S(s), z, B, h, w, out, (char*)ws, cap);
+  IRX_API_END
+}
+
+// ------------------------------------------------------------------ CLIP
+int irx_clip_workspace_bytes(const irx_model* m, int B, int L, size_t* bytes) {
+  IRX_API_BEGIN
+  IRX_CHECK(bytes && B > 0 && L > 0, "bad arguments");
+  *bytes = const_cast<Clip*>(as<Clip>(m, IRX_MODEL_CLIP))->workspace_bytes(B, L);
+  IRX_API_END
+}
+int irx_clip_encode(irx_model* m, void* s, const int* ids, int B, int L, void* out, void* ws, size_t cap) {
+  IRX_API_BEGIN
+  IRX_CHECK(ids && out && ws, "null buffer");
+  as<Clip>(m, IRX_MODEL_CLIP)->encode(S(s), ids, B, L, out, (char*)ws, cap);
+  IRX_API_END
+}
+
+// ------------------------------------------------------------------ scheduler / glue
+int irx_sched_step(void* s, const irx_step_params* p) {
+  IRX_API_BEGIN
+  IRX_CHECK(p, "null params");
+  StepArgs a;
+  a.dtype = p->dtype; a.B = p->batch; a.h = p->h; a.w = p->w;
+  a.eps = p->eps; a.cfg = p->cfg; a.guidance = p->guidance;
+  a.hist_store = p->hist_store;
+  for (int i = 0; i < 4; ++i) a.hist[i] = p->hist[i];
+  for (int i = 0; i < 5; ++i) a.hw[i] = p->hw[i];
+  a.e_div = p->e_div; a.e_mul = p->e_mul;
+  a.mode = p->mode; a.c0 = p->c0; a.c1 = p->c1; a.c2 = p->c2; a.c3 = p->c3;
+  a.x_src = p->x_src; a.cur_store = p->cur_store; a.x_out = p->x_out;
+  a.unet_in = p->unet_in; a.cin_pad = p->cin_pad; a.inpaint = p->inpaint; a.mask = p->mask; a.masked = p->masked;
+  sched_step(a, S(s));
+  IRX_API_END
+}
+int irx_pack_unet_input(void* s, int dtype, const float* lat, int B, int h, int w, int cfg, int cin_pad, int inpaint,
+                        const float* mask, const float* masked, void* out) {
+  IRX_API_BEGIN
+  IRX_CHECK(lat && out, "null buffer");
+  IRX_CHECK(!inpaint || (mask && masked && cin_pad >= 9), "inpaint inputs");
+  pack_unet_input(dtype, lat, B, h, w, cfg, cin_pad, inpaint, mask, masked, out, S(s));
+  IRX_API_END
+}
+int irx_latent_sample(void* s, int dtype, const void* mom, int B, int h, int w, const float* eps, const float* noise,
+                      int bcast, float sf, float a, float b, float* out) {
+  IRX_API_BEGIN
+  IRX_CHECK(mom && eps && out, "null buffer");
+  latent_sample(dtype, mom, 8, B, h, w, eps, noise, bcast, sf, a, b, out, S(s));
+  IRX_API_END
+}
+int irx_latents_to_vae(void* s, int dtype, const float* lat, int B, int h, int w, float sf, void* z) {
+  IRX_API_BEGIN
+  IRX_CHECK(lat && z, "null buffer");
+  scale_copy(dtype, lat, (long)B * h * w, sf, z, 4, 8, S(s));
+  IRX_API_END
+}
+int irx_image_to_tensor(void* s, int dtype, const uint8_t* img, const float* mask, int B, int H, int W, int cpad,
+                        void* out) {
+  IRX_API_BEGIN
+  IRX_CHECK(img && out && cpad >= 3, "bad arguments");
+  image_to_tensor(dtype, img, mask, B, H, W, cpad, out, S(s));
+  IRX_API_END
+}
+int irx_tensor_to_image(void* s, int dtype, const void* x, int B, int H, int W, int ldc, uint8_t* img, float* f01) {
+  IRX_API_BEGIN
+  IRX_CHECK(x && img && ldc >= 3, "bad arguments");
+  tensor_to_image(dtype, x, B, H, W, ldc, img, f01, S(s));
+  IRX_API_END
+}
+
+// ------------------------------------------------------------------ single ops
+int irx_op_conv2d(void* s, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hin, int win, int hv,
+                  int wv, const void* weight, const float* bias, int cout, int kh, int kw, int stride, int pad_t,
+                  int pad_l, int ho, int wo, const float* rowadd, long rowadd_ld, const void* residual, void* out,
+                  int out_f32, int act) {
+  IRX_API_BEGIN
+  GemmArgs a;
+  a.dtype = dtype;
+  a.conv = 1;
+  a.g.src0 = x0; a.g.src1 = x1; a.g.C0 = c0; a.g.C1 = c1;
+  a.g.N = n; a.g.Hin = hin; a.g.Win = win; a.g.Hv = hv; a.g.Wv = wv;
+  a.g.KH = kh; a.g.KW = kw; a.g.stride = stride; a.g.pad_t = pad_t; a.g.pad_l = pad_l; a.g.Ho = ho; a.g.Wo = wo;
+  a.M = n * ho * wo; a.N = cout; a.K = kh * kw * (c0 + c1);
+  a.B = weight; a.ldb = a.K;
+  a.C = out; a.ldc = cout; a.out_f32 = out_f32;
+  a.bias = bias;
+  a.rowadd = rowadd; a.rowadd_ld = rowadd_ld; a.rows_per_group = ho * wo;
+  a.residual = residual; a.ldr = cout;
+  a.act = act;
+  gemm(a, S(s));
+  IRX_API_END
+}
+
+int irx_op_gemm(void* s, int dtype, int M, int N, int K, const void* A, long lda, const void* B, long ldb, void* C,
+                long ldc, const float* bias, float alpha, int act, const void* residual, long ldr, int out_f32,
+                int batch, long sA, long sB, long sC, long sR) {
+  IRX_API_BEGIN
+  GemmArgs a;
+  a.dtype = dtype; a.M = M; a.N = N; a.K = K;
+  a.A = A; a.lda = lda; a.sA = sA;
+  a.B = B; a.ldb = ldb; a.sB = sB;
+  a.C = C; a.ldc = ldc; a.sC = sC;
+  a.bias = bias; a.alpha = alpha; a.act = act;
+  a.residual = residual; a.ldr = ldr; a.sR = sR;
+  a.out_f32 = out_f32;
+  a.batch = batch > 0 ? batch : 1;
+  gemm(a, S(s));
+  IRX_API_END
+}
+
+int irx_op_group_norm(void* s, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hw, int groups,
+                      float eps, const float* gamma, const float* beta, int silu, void* out, void* ws) {
+  IRX_API_BEGIN
+  IRX_CHECK(x0 && gamma && beta && out && ws, "null buffer");
+  group_norm(dtype, x0, x1, c0, c1, n, hw, groups, eps, gamma, beta, silu, out, ws, S(s));
+  IRX_API_END
+}
+size_t irx_op_group_norm_ws_bytes(int n, int hw, int groups) { return gn_ws_bytes(n, hw, groups); }
+
+int irx_op_layer_norm(void* s, int dtype, const void* x, int rows, int c, float eps, const float* gamma,
+                      const float* beta, void* out) {
+  IRX_API_BEGIN
+  IRX_CHECK(x && gamma && beta && out, "null buffer");
+  layer_norm(dtype, x, c, rows, c, eps, gamma, beta, out, c, S(s));
+  IRX_API_END
+}
+
+int irx_op_attention(void* s, int dtype, int B, int H, int lq, int lk, int d, const void* q, long ldq, long sq,
+                     const void* k, long ldk, long sk, const void* v, long ldv, long sv, void* o, long ldo, long so,
+                     float scale, int causal) {
+  IRX_API_BEGIN
+  AttnArgs a;
+  a.dtype = dtype; a.B = B; a.H = H; a.Lq = lq; a.Lk = lk; a.d = d;
+  a.q = q; a.ldq = ldq; a.sq = sq;
+  a.k = k; a.ldk = ldk; a.sk = sk;
+  a.v = v; a.ldv = ldv; a.sv = sv;
+  a.o = o; a.ldo = ldo; a.so = so;
+  a.scale = scale; a.causal = causal;
+  attention(a, S(s));
+  IRX_API_END
+}
+
+int irx_op_geglu(void* s, int dtype, const void* proj, int M, int F, void* out) {
+  IRX_API_BEGIN
+  IRX_CHECK(proj && out, "null buffer");
+  geglu(dtype, proj, 2L * F, M, F, out, F, S(s));
+  IRX_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+// irx — MI355X-native SD-1.5 restoration engine: shared device/host helpers.
+// gfx950 (CDNA4) only: wave64, MFMA 16x16 tiles, NHWC activations.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <string>
+
+namespace irx {
+
+enum DType : int { F32 = 0, BF16 = 1 };
+
+typedef uint16_t bf16_t;   // storage type for bfloat16
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+
+// ---------------------------------------------------------------- conversions
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;                       // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return __builtin_bit_cast(bf16_t, b);
+}
+template <typename T> __device__ __forceinline__ float ld_f(const T* p);
+template <> __device__ __forceinline__ float ld_f<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld_f<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <typename T> __device__ __forceinline__ T from_f(float f);
+template <> __device__ __forceinline__ float from_f<float>(float f) { return f; }
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float f) { return f2bf(f); }
+
+// 16-byte vector <-> floats
+template <typename T> struct Vec16;
+template <> struct Vec16<float> {
+  static constexpr int N = 4;
+  __device__ static void unpack(const uint4& u, float* f) {
+    f[0] = __uint_as_float(u.x); f[1] = __uint_as_float(u.y);
+    f[2] = __uint_as_float(u.z); f[3] = __uint_as_float(u.w);
+  }
+  __device__ static uint4 pack(const float* f) {
+    return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+  }
+};
+template <> struct Vec16<bf16_t> {
+  static constexpr int N = 8;
+  __device__ static void unpack(const uint4& u, float* f) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(w[i] << 16);
+      f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ static uint4 pack(const float* f) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+
+// ---------------------------------------------------------------- activations (epilogues)
+enum ActKind : int { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_QUICK_GELU = 3 };
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float apply_act(float x, int act) {
+  switch (act) {
+    case ACT_SILU: return silu_f(x);
+    case ACT_GELU: return gelu_erf(x);
+    case ACT_QUICK_GELU: return x / (1.0f + __expf(-1.702f * x));
+    default: return x;
+  }
+}
+
+// ---------------------------------------------------------------- XCD-aware block remap (bijective)
+// Consecutive logical tiles land on the same XCD (blocks b, b+8, ... share one), so tiles that
+// share an operand panel hit the same 4 MiB L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+// ---------------------------------------------------------------- host-side errors
+void set_error(const std::string& msg);
+const char* last_error();
+
+struct Error : public std::exception {
+  std::string msg;
+  explicit Error(std::string m) : msg(std::move(m)) {}
+  const char* what() const noexcept override { return msg.c_str(); }
+};
+#define IRX_CHECK(cond, msg)                                                          \
+  do {                                                                                 \
+    if (!(cond)) throw ::irx::Error(std::string(__func__) + ": " + (msg));           \
+  } while (0)
+#define IRX_HIP(call)                                                                 \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      throw ::irx::Error(std::string(#call) + " failed: " + hipGetErrorString(e_));   \
+  } while (0)
+#define IRX_LAUNCH_CHECK() IRX_HIP(hipGetLastError())
+
+inline size_t dsize(int dt) { return dt == F32 ? 4 : 2; }
+
+}  // namespace irx

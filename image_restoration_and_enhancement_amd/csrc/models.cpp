@@ -1,0 +1,786 @@
+// irx — native model graphs for the SD-1.5 restoration hot path.
+//
+// Each class registers its parameters under the diffusers / transformers names (the manifest the
+// host packs weights by) and runs its forward pass as a sequence of irx kernel launches on one
+// stream, with every temporary carved from a caller-provided workspace by a deterministic
+// allocator (a dry run with no launches sizes the workspace).
+//   Unet  — diffusers UNet2DConditionModel (SD-1.5 config, outputs/models/*/best/unet/config.json)
+//   Vae   — diffusers AutoencoderKL encoder (+quant_conv) / decoder (+post_quant_conv)
+//   Clip  — transformers CLIPTextModel (last_hidden_state)
+// Fusions relative to the module-by-module reference: GroupNorm+SiLU in one pass; conv bias,
+// time-embedding add and residual add in the conv/GEMM epilogues; q|k|v as one GEMM; every
+// resnet's time_emb_proj as one GEMM per step; every cross-attention K|V projection as one GEMM
+// per prompt (constant over the denoising loop); Upsample2D's nearest resize and the up-block
+// skip concat folded into the following convolution's operand gather.
+#include "models.h"
+
+#include <cmath>
+
+namespace irx {
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------------------------------------- Arena
+void* Arena::alloc(size_t bytes) {
+  bytes = align_up(bytes ? bytes : 1, 256);
+  size_t off = (size_t)-1;
+  for (auto it = free_.begin(); it != free_.end(); ++it) {
+    if (it->second >= bytes) {
+      off = it->first;
+      const size_t rest = it->second - bytes;
+      free_.erase(it);
+      if (rest) free_[off + bytes] = rest;
+      break;
+    }
+  }
+  if (off == (size_t)-1) {
+    off = end_;
+    end_ += bytes;
+    if (end_ > peak_) peak_ = end_;
+  }
+  if (base_ && end_ > cap_) throw Error("workspace too small: need > " + std::to_string(end_) + " bytes");
+  live_[off] = bytes;
+  return base_ ? (void*)(base_ + off) : (void*)(uintptr_t)(off + 4096);
+}
+
+void Arena::free(void* p) {
+  if (!p) return;
+  const size_t off = base_ ? (size_t)((char*)p - base_) : (size_t)((uintptr_t)p - 4096);
+  auto it = live_.find(off);
+  if (it == live_.end()) throw Error("workspace: double free");
+  size_t o = off, sz = it->second;
+  live_.erase(it);
+  auto nx = free_.lower_bound(o);
+  if (nx != free_.end() && nx->first == o + sz) { sz += nx->second; free_.erase(nx); }
+  auto pv = free_.lower_bound(o);
+  if (pv != free_.begin()) {
+    --pv;
+    if (pv->first + pv->second == o) { o = pv->first; sz += pv->second; free_.erase(pv); }
+  }
+  if (o + sz == end_) end_ = o;
+  else free_[o] = sz;
+}
+
+// ---------------------------------------------------------------------------------------------- Model
+P Model::reg(const std::string& name, int layout, int dtype, std::vector<int64_t> shape) {
+  int64_t n = 1;
+  for (auto d : shape) n *= d;
+  ParamEntry e{name, layout, dtype, shape, blob_bytes_, (size_t)n * dsize(dtype)};
+  params_.push_back(e);
+  P p;
+  p.off = blob_bytes_;
+  p.set = true;
+  blob_bytes_ = align_up(blob_bytes_ + e.bytes, 256);
+  return p;
+}
+
+void Model::bind(void* blob, size_t bytes) {
+  IRX_CHECK(blob != nullptr, "null weight blob");
+  IRX_CHECK(bytes >= blob_bytes_, "weight blob too small: " + std::to_string(bytes) + " < " + std::to_string(blob_bytes_));
+  IRX_CHECK(((uintptr_t)blob % 256) == 0, "weight blob must be 256-byte aligned");
+  blob_ = (char*)blob;
+}
+
+Act Model::new_act(Ctx& c, int n, int h, int w, int ch) {
+  Act a;
+  a.n = n; a.h = h; a.w = w; a.c = ch;
+  a.p = c.ws->alloc((size_t)n * h * w * ch * dsize(dt_));
+  return a;
+}
+
+void Model::conv2d(Ctx& c, const Act& x0, const Act* x1, P w, P b, int cout, int k, int stride, int pad_t,
+                   int pad_l, int hv, int wv, const Act& out, const float* rowadd, long rowadd_ld,
+                   const void* residual, int out_f32, int ldc) {
+  if (c.ws->dry()) return;
+  GemmArgs a;
+  a.dtype = dt_;
+  a.conv = 1;
+  a.g.src0 = x0.p; a.g.C0 = x0.c;
+  a.g.src1 = x1 ? x1->p : nullptr; a.g.C1 = x1 ? x1->c : 0;
+  a.g.N = x0.n; a.g.Hin = x0.h; a.g.Win = x0.w; a.g.Hv = hv; a.g.Wv = wv;
+  a.g.KH = k; a.g.KW = k; a.g.stride = stride; a.g.pad_t = pad_t; a.g.pad_l = pad_l;
+  a.g.Ho = out.h; a.g.Wo = out.w;
+  a.M = out.n * out.h * out.w;
+  a.N = cout;
+  a.K = k * k * (a.g.C0 + a.g.C1);
+  a.B = ptr(w); a.ldb = a.K;
+  a.C = out.p; a.ldc = ldc < 0 ? cout : ldc;
+  a.out_f32 = out_f32;
+  a.bias = b.set ? fptr(b) : nullptr;
+  a.rowadd = rowadd; a.rowadd_ld = rowadd_ld; a.rows_per_group = out.h * out.w;
+  a.residual = residual; a.ldr = a.ldc;
+  gemm(a, c.s);
+}
+
+void Model::linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, const float* bias, void* C, long ldc,
+                   int act, const void* residual, long ldr, int out_f32) {
+  if (c.ws->dry()) return;
+  GemmArgs a;
+  a.dtype = dt_;
+  a.M = M; a.N = N; a.K = K;
+  a.A = A; a.lda = lda;
+  a.B = ptr(w); a.ldb = K;
+  a.C = C; a.ldc = ldc;
+  a.bias = bias;
+  a.act = act;
+  a.residual = residual; a.ldr = ldr;
+  a.out_f32 = out_f32;
+  gemm(a, c.s);
+}
+
+void Model::gnorm(Ctx& c, const Act& x0, const Act* x1, P g, P b, float eps, int silu, const Act& out) {
+  void* ws = c.ws->alloc(gn_ws_bytes(x0.n, x0.h * x0.w, cfg_.norm_groups));
+  if (!c.ws->dry())
+    group_norm(dt_, x0.p, x1 ? x1->p : nullptr, x0.c, x1 ? x1->c : 0, x0.n, x0.h * x0.w, cfg_.norm_groups, eps,
+               fptr(g), fptr(b), silu, out.p, ws, c.s);
+  c.ws->free(ws);
+}
+
+void Model::lnorm(Ctx& c, const void* x, int rows, int C, P g, P b, float eps, void* out) {
+  if (c.ws->dry()) return;
+  layer_norm(dt_, x, C, rows, C, eps, fptr(g), fptr(b), out, C, c.s);
+}
+
+static std::string join(const std::vector<std::string>& v) {
+  std::string s;
+  for (size_t i = 0; i < v.size(); ++i) s += (i ? "|" : "") + v[i];
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------------- UNet
+ResW Unet::make_res(const std::string& p, int cin, int cout) {
+  ResW r;
+  r.cin = cin; r.cout = cout;
+  r.n1w = vec(p + "norm1.weight", cin); r.n1b = vec(p + "norm1.bias", cin);
+  r.c1w = conv(p + "conv1.weight", cout, 3, 3, cin); r.c1b = vec(p + "conv1.bias", cout);
+  r.temb_off = temb_cols_;
+  temb_cols_ += cout;
+  temb_names_w_.push_back(p + "time_emb_proj.weight");
+  temb_names_b_.push_back(p + "time_emb_proj.bias");
+  r.n2w = vec(p + "norm2.weight", cout); r.n2b = vec(p + "norm2.bias", cout);
+  r.c2w = conv(p + "conv2.weight", cout, 3, 3, cout); r.c2b = vec(p + "conv2.bias", cout);
+  r.shortcut = cin != cout;
+  if (r.shortcut) { r.scw = mat(p + "conv_shortcut.weight", cout, cin); r.scb = vec(p + "conv_shortcut.bias", cout); }
+  return r;
+}
+
+Unet::XfW Unet::make_xf(const std::string& p, int c) {
+  XfW a;
+  a.c = c;
+  const std::string b = p + "transformer_blocks.0.";
+  a.nw = vec(p + "norm.weight", c); a.nb = vec(p + "norm.bias", c);
+  a.piw = mat(p + "proj_in.weight", c, c); a.pib = vec(p + "proj_in.bias", c);
+  a.ln1w = vec(b + "norm1.weight", c); a.ln1b = vec(b + "norm1.bias", c);
+  a.qkvw = mat(b + "attn1.to_q.weight|" + b + "attn1.to_k.weight|" + b + "attn1.to_v.weight", 3 * c, c);
+  a.o1w = mat(b + "attn1.to_out.0.weight", c, c); a.o1b = vec(b + "attn1.to_out.0.bias", c);
+  a.ln2w = vec(b + "norm2.weight", c); a.ln2b = vec(b + "norm2.bias", c);
+  a.q2w = mat(b + "attn2.to_q.weight", c, c);
+  a.kv_off = kv_cols_;
+  kv_cols_ += 2 * c;
+  kv_names_.push_back(b + "attn2.to_k.weight");
+  kv_names_.push_back(b + "attn2.to_v.weight");
+  a.o2w = mat(b + "attn2.to_out.0.weight", c, c); a.o2b = vec(b + "attn2.to_out.0.bias", c);
+  a.ln3w = vec(b + "norm3.weight", c); a.ln3b = vec(b + "norm3.bias", c);
+  a.ffw = mat(b + "ff.net.0.proj.weight", 8 * c, c); a.ffb = vec(b + "ff.net.0.proj.bias", 8 * c);
+  a.ff2w = mat(b + "ff.net.2.weight", c, 4 * c); a.ff2b = vec(b + "ff.net.2.bias", c);
+  a.pow = mat(p + "proj_out.weight", c, c); a.pob = vec(p + "proj_out.bias", c);
+  return a;
+}
+
+Unet::Unet(const irx_model_config& cfg, int dtype) : Model(IRX_MODEL_UNET, cfg, dtype) {
+  IRX_CHECK(cfg.n_blocks >= 2 && cfg.n_blocks <= 8, "bad UNet block count");
+  IRX_CHECK(cfg.heads > 0 && cfg.norm_groups > 0, "bad UNet config");
+  const int* bo = cfg.block_out_channels;
+  const int nb = cfg.n_blocks;
+  cin_pad_ = (cfg.in_channels + 7) / 8 * 8;
+  temb_dim_ = bo[0] * 4;
+  conv_in_w = conv("conv_in.weight", bo[0], 3, 3, cin_pad_);
+  conv_in_b = vec("conv_in.bias", bo[0]);
+  t1w = mat("time_embedding.linear_1.weight", temb_dim_, bo[0]); t1b = vec("time_embedding.linear_1.bias", temb_dim_);
+  t2w = mat("time_embedding.linear_2.weight", temb_dim_, temb_dim_); t2b = vec("time_embedding.linear_2.bias", temb_dim_);
+  int cout = bo[0];
+  for (int i = 0; i < nb; ++i) {
+    Block blk;
+    const int cin = cout;
+    cout = bo[i];
+    blk.ch = cout;
+    blk.has_attn = cfg.down_attn[i] != 0;
+    for (int j = 0; j < cfg.layers_per_block; ++j) {
+      const std::string p = "down_blocks." + std::to_string(i) + ".";
+      blk.res.push_back(make_res(p + "resnets." + std::to_string(j) + ".", j == 0 ? cin : cout, cout));
+      if (blk.has_attn) blk.attn.push_back(make_xf(p + "attentions." + std::to_string(j) + ".", cout));
+    }
+    blk.resample = i < nb - 1;
+    if (blk.resample) {
+      const std::string p = "down_blocks." + std::to_string(i) + ".downsamplers.0.conv.";
+      blk.rsw = conv(p + "weight", cout, 3, 3, cout); blk.rsb = vec(p + "bias", cout);
+    }
+    down_.push_back(blk);
+  }
+  const int c = bo[nb - 1];
+  mid_res0_ = make_res("mid_block.resnets.0.", c, c);
+  mid_attn_ = make_xf("mid_block.attentions.0.", c);
+  mid_res1_ = make_res("mid_block.resnets.1.", c, c);
+  // up path: diffusers channel bookkeeping (prev_output_channel / res_skip_channels)
+  int out_ch = bo[nb - 1];
+  for (int i = 0; i < nb; ++i) {
+    Block blk;
+    const int prev = out_ch;
+    out_ch = bo[nb - 1 - i];
+    const int in_ch = bo[std::max(nb - 2 - i, 0)];
+    blk.ch = out_ch;
+    blk.has_attn = cfg.up_attn[i] != 0;
+    for (int j = 0; j <= cfg.layers_per_block; ++j) {
+      const int skip = j == cfg.layers_per_block ? in_ch : out_ch;
+      const int rin = j == 0 ? prev : out_ch;
+      const std::string p = "up_blocks." + std::to_string(i) + ".";
+      blk.res.push_back(make_res(p + "resnets." + std::to_string(j) + ".", rin + skip, out_ch));
+      if (blk.has_attn) blk.attn.push_back(make_xf(p + "attentions." + std::to_string(j) + ".", out_ch));
+    }
+    blk.resample = i < nb - 1;
+    if (blk.resample) {
+      const std::string p = "up_blocks." + std::to_string(i) + ".upsamplers.0.conv.";
+      blk.rsw = conv(p + "weight", out_ch, 3, 3, out_ch); blk.rsb = vec(p + "bias", out_ch);
+    }
+    up_.push_back(blk);
+  }
+  nout_w = vec("conv_norm_out.weight", bo[0]); nout_b = vec("conv_norm_out.bias", bo[0]);
+  conv_out_w = conv("conv_out.weight", cfg.out_channels, 3, 3, bo[0]);
+  conv_out_b = vec("conv_out.bias", cfg.out_channels);
+  // fused projections
+  tpw = mat(join(temb_names_w_), temb_cols_, temb_dim_);
+  tpb = vec(join(temb_names_b_), temb_cols_);
+  kvw = mat(join(kv_names_), kv_cols_, cfg.cross_attention_dim);
+}
+
+Act Unet::resnet(Ctx& c, const ResW& r, Act& x0, Act* x1, const float* tproj, float eps) {
+  const int B = x0.n, H = x0.h, W = x0.w;
+  const int cin = x0.c + (x1 ? x1->c : 0);
+  IRX_CHECK(cin == r.cin, "resnet channel mismatch");
+  Act gn1 = new_act(c, B, H, W, cin);
+  gnorm(c, x0, x1, r.n1w, r.n1b, eps, 1, gn1);
+  Act h1 = new_act(c, B, H, W, r.cout);
+  conv2d(c, gn1, nullptr, r.c1w, r.c1b, r.cout, 3, 1, 1, 1, H, W, h1, tproj ? tproj + r.temb_off : nullptr,
+         temb_cols_);
+  drop(c, gn1);
+  Act gn2 = new_act(c, B, H, W, r.cout);
+  gnorm(c, h1, nullptr, r.n2w, r.n2b, eps, 1, gn2);
+  drop(c, h1);
+  Act sc;
+  const void* res = x0.p;
+  if (r.shortcut) {
+    sc = new_act(c, B, H, W, r.cout);
+    conv2d(c, x0, x1, r.scw, r.scb, r.cout, 1, 1, 0, 0, H, W, sc);
+    res = sc.p;
+  }
+  Act out = new_act(c, B, H, W, r.cout);
+  conv2d(c, gn2, nullptr, r.c2w, r.c2b, r.cout, 3, 1, 1, 1, H, W, out, nullptr, 0, res);
+  drop(c, gn2);
+  if (r.shortcut) drop(c, sc);
+  return out;
+}
+
+Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
+  const int B = x.n, HW = x.h * x.w, C = a.c;
+  const long M = (long)B * HW;
+  const size_t es = dsize(dt_);
+  const int heads = cfg_.heads, d = C / heads;
+  const float scale = 1.0f / std::sqrt((float)d);
+  Act gn = new_act(c, B, x.h, x.w, C);
+  gnorm(c, x, nullptr, a.nw, a.nb, 1e-6f, 0, gn);
+  Act h = new_act(c, B, x.h, x.w, C);
+  linear(c, gn.p, C, M, C, a.piw, C, fptr(a.pib), h.p, C);
+  drop(c, gn);
+  void* n = c.ws->alloc(M * C * es);
+  void* att = c.ws->alloc(M * C * es);
+  // self-attention
+  lnorm(c, h.p, M, C, a.ln1w, a.ln1b, 1e-5f, n);
+  void* qkv = c.ws->alloc(M * 3 * C * es);
+  linear(c, n, C, M, C, a.qkvw, 3 * C, nullptr, qkv, 3 * C);
+  if (!c.ws->dry()) {
+    AttnArgs aa;
+    aa.dtype = dt_; aa.B = B; aa.H = heads; aa.Lq = HW; aa.Lk = HW; aa.d = d; aa.scale = scale;
+    aa.q = qkv; aa.ldq = 3 * C; aa.sq = (long)HW * 3 * C;
+    aa.k = (char*)qkv + C * es; aa.ldk = 3 * C; aa.sk = aa.sq;
+    aa.v = (char*)qkv + 2 * C * es; aa.ldv = 3 * C; aa.sv = aa.sq;
+    aa.o = att; aa.ldo = C; aa.so = (long)HW * C;
+    attention(aa, c.s);
+  }
+  c.ws->free(qkv);
+  linear(c, att, C, M, C, a.o1w, C, fptr(a.o1b), h.p, C, ACT_NONE, h.p, C);
+  // cross-attention (K|V precomputed per prompt)
+  lnorm(c, h.p, M, C, a.ln2w, a.ln2b, 1e-5f, n);
+  linear(c, n, C, M, C, a.q2w, C, nullptr, att, C);
+  if (!c.ws->dry()) {
+    AttnArgs aa;
+    aa.dtype = dt_; aa.B = B; aa.H = heads; aa.Lq = HW; aa.Lk = L; aa.d = d; aa.scale = scale;
+    aa.q = att; aa.ldq = C; aa.sq = (long)HW * C;
+    aa.k = (const char*)kv + a.kv_off * es; aa.ldk = kv_cols_; aa.sk = (long)L * kv_cols_;
+    aa.v = (const char*)kv + (a.kv_off + C) * es; aa.ldv = kv_cols_; aa.sv = aa.sk;
+    aa.o = n; aa.ldo = C; aa.so = (long)HW * C;
+    attention(aa, c.s);
+  }
+  linear(c, n, C, M, C, a.o2w, C, fptr(a.o2b), h.p, C, ACT_NONE, h.p, C);
+  // GEGLU feed-forward
+  lnorm(c, h.p, M, C, a.ln3w, a.ln3b, 1e-5f, n);
+  void* ff = c.ws->alloc(M * 8 * C * es);
+  linear(c, n, C, M, C, a.ffw, 8 * C, fptr(a.ffb), ff, 8 * C);
+  void* g = c.ws->alloc(M * 4 * C * es);
+  if (!c.ws->dry()) geglu(dt_, ff, 8 * C, M, 4 * C, g, 4 * C, c.s);
+  c.ws->free(ff);
+  linear(c, g, 4 * C, M, 4 * C, a.ff2w, C, fptr(a.ff2b), h.p, C, ACT_NONE, h.p, C);
+  c.ws->free(g);
+  c.ws->free(att);
+  c.ws->free(n);
+  Act out = new_act(c, B, x.h, x.w, C);
+  linear(c, h.p, C, M, C, a.pow, C, fptr(a.pob), out.p, C, ACT_NONE, x.p, C);
+  drop(c, h);
+  return out;
+}
+
+void Unet::run(Ctx& c, const void* x, int B, int h, int w, const float* t, const void* kv, int L, float* eps_out) {
+  const int* bo = cfg_.block_out_channels;
+  const float eps = cfg_.norm_eps;
+  const size_t es = dsize(dt_);
+  // time embedding: sinusoid -> linear_1 -> SiLU -> linear_2, then SiLU(emb) (every resnet's input) and all
+  // resnets' time_emb_proj in one GEMM
+  void* te0 = c.ws->alloc((size_t)B * bo[0] * es);
+  void* te1 = c.ws->alloc((size_t)B * temb_dim_ * es);
+  void* te2 = c.ws->alloc((size_t)B * temb_dim_ * es);
+  float* tproj = (float*)c.ws->alloc((size_t)B * temb_cols_ * sizeof(float));
+  if (!c.ws->dry()) timestep_embed(dt_, t, B, bo[0], cfg_.flip_sin_to_cos, cfg_.freq_shift, te0, c.s);
+  linear(c, te0, bo[0], B, bo[0], t1w, temb_dim_, fptr(t1b), te1, temb_dim_, ACT_SILU);
+  linear(c, te1, temb_dim_, B, temb_dim_, t2w, temb_dim_, fptr(t2b), te2, temb_dim_, ACT_SILU);
+  linear(c, te2, temb_dim_, B, temb_dim_, tpw, temb_cols_, fptr(tpb), tproj, temb_cols_, ACT_NONE, nullptr, 0, 1);
+  c.ws->free(te0);
+  c.ws->free(te1);
+  c.ws->free(te2);
+
+  Act xin;
+  xin.p = const_cast<void*>(x); xin.n = B; xin.h = h; xin.w = w; xin.c = cin_pad_;
+  Act cur = new_act(c, B, h, w, bo[0]);
+  conv2d(c, xin, nullptr, conv_in_w, conv_in_b, bo[0], 3, 1, 1, 1, h, w, cur);
+  std::vector<Act> skips{cur};
+  bool cur_is_skip = true;
+  for (auto& blk : down_) {
+    for (size_t j = 0; j < blk.res.size(); ++j) {
+      Act nx = resnet(c, blk.res[j], cur, nullptr, tproj, eps);
+      if (!cur_is_skip) drop(c, cur);
+      if (blk.has_attn) {
+        Act t2 = transformer(c, blk.attn[j], nx, kv, L);
+        drop(c, nx);
+        nx = t2;
+      }
+      skips.push_back(nx);
+      cur = nx;
+      cur_is_skip = true;
+    }
+    if (blk.resample) {
+      const int Ho = (cur.h - 1) / 2 + 1, Wo = (cur.w - 1) / 2 + 1;
+      Act d = new_act(c, B, Ho, Wo, blk.ch);
+      conv2d(c, cur, nullptr, blk.rsw, blk.rsb, blk.ch, 3, 2, 1, 1, cur.h, cur.w, d);
+      skips.push_back(d);
+      cur = d;
+    }
+  }
+  {
+    Act r = resnet(c, mid_res0_, cur, nullptr, tproj, eps);
+    Act a = transformer(c, mid_attn_, r, kv, L);
+    drop(c, r);
+    cur = resnet(c, mid_res1_, a, nullptr, tproj, eps);
+    drop(c, a);
+  }
+  for (auto& blk : up_) {
+    for (size_t j = 0; j < blk.res.size(); ++j) {
+      Act skip = skips.back();
+      skips.pop_back();
+      Act nx = resnet(c, blk.res[j], cur, &skip, tproj, eps);
+      drop(c, cur);
+      drop(c, skip);
+      if (blk.has_attn) {
+        Act t2 = transformer(c, blk.attn[j], nx, kv, L);
+        drop(c, nx);
+        nx = t2;
+      }
+      cur = nx;
+    }
+    if (blk.resample) {
+      // Upsample2D: nearest resize to the next skip's size (== 2x unless a latent side is not /8)
+      const int th = skips.back().h, tw = skips.back().w;
+      Act u = new_act(c, B, th, tw, blk.ch);
+      conv2d(c, cur, nullptr, blk.rsw, blk.rsb, blk.ch, 3, 1, 1, 1, th, tw, u);
+      drop(c, cur);
+      cur = u;
+    }
+  }
+  Act gn = new_act(c, B, h, w, bo[0]);
+  gnorm(c, cur, nullptr, nout_w, nout_b, eps, 1, gn);
+  drop(c, cur);
+  Act o;
+  o.p = eps_out; o.n = B; o.h = h; o.w = w; o.c = cfg_.out_channels;
+  conv2d(c, gn, nullptr, conv_out_w, conv_out_b, cfg_.out_channels, 3, 1, 1, 1, h, w, o, nullptr, 0, nullptr, 1);
+  drop(c, gn);
+  c.ws->free(tproj);
+}
+
+size_t Unet::workspace_bytes(int B, int h, int w) {
+  Arena ar;
+  ar.reset(nullptr, 0);
+  Ctx c{nullptr, &ar};
+  run(c, nullptr, B, h, w, nullptr, nullptr, 77, nullptr);
+  return ar.peak();
+}
+
+void Unet::forward(hipStream_t s, const void* x, int B, int h, int w, const float* t, const void* kv, int L,
+                   float* eps, char* ws, size_t cap) {
+  IRX_CHECK(blob_, "weights not bound");
+  Arena ar;
+  ar.reset(ws, cap);
+  Ctx c{s, &ar};
+  run(c, x, B, h, w, t, kv, L, eps);
+}
+
+void Unet::prepare_context(hipStream_t s, const void* ctx, int B, int L, void* kv, char* ws, size_t cap) {
+  IRX_CHECK(blob_, "weights not bound");
+  (void)ws; (void)cap;
+  Arena ar;
+  ar.reset(ws ? ws : (char*)16, cap);   // no temporaries needed
+  Ctx c{s, &ar};
+  linear(c, ctx, cfg_.cross_attention_dim, B * L, cfg_.cross_attention_dim, kvw, kv_cols_, nullptr, kv, kv_cols_);
+}
+
+// ---------------------------------------------------------------------------------------------- VAE
+ResW Vae::make_res(const std::string& p, int cin, int cout) {
+  ResW r;
+  r.cin = cin; r.cout = cout;
+  r.n1w = vec(p + "norm1.weight", cin); r.n1b = vec(p + "norm1.bias", cin);
+  r.c1w = conv(p + "conv1.weight", cout, 3, 3, cin); r.c1b = vec(p + "conv1.bias", cout);
+  r.n2w = vec(p + "norm2.weight", cout); r.n2b = vec(p + "norm2.bias", cout);
+  r.c2w = conv(p + "conv2.weight", cout, 3, 3, cout); r.c2b = vec(p + "conv2.bias", cout);
+  r.shortcut = cin != cout;
+  if (r.shortcut) { r.scw = mat(p + "conv_shortcut.weight", cout, cin); r.scb = vec(p + "conv_shortcut.bias", cout); }
+  return r;
+}
+
+Vae::AttW Vae::make_attn(const std::string& p, int c) {
+  AttW a;
+  a.c = c;
+  a.gw = vec(p + "group_norm.weight", c); a.gb = vec(p + "group_norm.bias", c);
+  a.qkvw = mat(p + "to_q.weight|" + p + "to_k.weight|" + p + "to_v.weight", 3 * c, c);
+  a.qkvb = vec(p + "to_q.bias|" + p + "to_k.bias|" + p + "to_v.bias", 3 * c);
+  a.ow = mat(p + "to_out.0.weight", c, c); a.ob = vec(p + "to_out.0.bias", c);
+  return a;
+}
+
+Vae::Vae(const irx_model_config& cfg, int dtype) : Model(IRX_MODEL_VAE, cfg, dtype) {
+  const int* bo = cfg.block_out_channels;
+  const int nb = cfg.n_blocks;
+  const int L = cfg.latent_channels;
+  IRX_CHECK(L <= 4 && cfg.in_channels <= 8 && cfg.out_channels <= 4, "VAE channel counts out of range");
+  e_cin_w = conv("encoder.conv_in.weight", bo[0], 3, 3, 8); e_cin_b = vec("encoder.conv_in.bias", bo[0]);
+  int cout = bo[0];
+  for (int i = 0; i < nb; ++i) {
+    const int cin = cout;
+    cout = bo[i];
+    std::vector<ResW> rs;
+    for (int j = 0; j < cfg.layers_per_block; ++j)
+      rs.push_back(make_res("encoder.down_blocks." + std::to_string(i) + ".resnets." + std::to_string(j) + ".",
+                            j == 0 ? cin : cout, cout));
+    e_res_.push_back(rs);
+    if (i < nb - 1) {
+      const std::string p = "encoder.down_blocks." + std::to_string(i) + ".downsamplers.0.conv.";
+      e_down_w_.push_back(conv(p + "weight", cout, 3, 3, cout));
+      e_down_b_.push_back(vec(p + "bias", cout));
+    }
+  }
+  const int c = bo[nb - 1];
+  e_mid0_ = make_res("encoder.mid_block.resnets.0.", c, c);
+  e_att_ = make_attn("encoder.mid_block.attentions.0.", c);
+  e_mid1_ = make_res("encoder.mid_block.resnets.1.", c, c);
+  e_nout_w = vec("encoder.conv_norm_out.weight", c); e_nout_b = vec("encoder.conv_norm_out.bias", c);
+  e_cout_w = conv("encoder.conv_out.weight", 8, 3, 3, c); e_cout_b = vec("encoder.conv_out.bias", 8);
+  qw = mat("quant_conv.weight", 8, 8); qb = vec("quant_conv.bias", 8);
+  pqw = mat("post_quant_conv.weight", 8, 8); pqb = vec("post_quant_conv.bias", 8);
+  d_cin_w = conv("decoder.conv_in.weight", c, 3, 3, 8); d_cin_b = vec("decoder.conv_in.bias", c);
+  d_mid0_ = make_res("decoder.mid_block.resnets.0.", c, c);
+  d_att_ = make_attn("decoder.mid_block.attentions.0.", c);
+  d_mid1_ = make_res("decoder.mid_block.resnets.1.", c, c);
+  int out_ch = bo[nb - 1];
+  for (int i = 0; i < nb; ++i) {
+    const int prev = out_ch;
+    out_ch = bo[nb - 1 - i];
+    std::vector<ResW> rs;
+    for (int j = 0; j <= cfg.layers_per_block; ++j)
+      rs.push_back(make_res("decoder.up_blocks." + std::to_string(i) + ".resnets." + std::to_string(j) + ".",
+                            j == 0 ? prev : out_ch, out_ch));
+    d_res_.push_back(rs);
+    if (i < nb - 1) {
+      const std::string p = "decoder.up_blocks." + std::to_string(i) + ".upsamplers.0.conv.";
+      d_up_w_.push_back(conv(p + "weight", out_ch, 3, 3, out_ch));
+      d_up_b_.push_back(vec(p + "bias", out_ch));
+    }
+  }
+  d_nout_w = vec("decoder.conv_norm_out.weight", bo[0]); d_nout_b = vec("decoder.conv_norm_out.bias", bo[0]);
+  d_cout_w = conv("decoder.conv_out.weight", 4, 3, 3, bo[0]); d_cout_b = vec("decoder.conv_out.bias", 4);
+}
+
+Act Vae::resnet(Ctx& c, const ResW& r, Act& x) {
+  const float eps = cfg_.norm_eps;
+  const int B = x.n, H = x.h, W = x.w;
+  Act gn1 = new_act(c, B, H, W, r.cin);
+  gnorm(c, x, nullptr, r.n1w, r.n1b, eps, 1, gn1);
+  Act h1 = new_act(c, B, H, W, r.cout);
+  conv2d(c, gn1, nullptr, r.c1w, r.c1b, r.cout, 3, 1, 1, 1, H, W, h1);
+  drop(c, gn1);
+  Act gn2 = new_act(c, B, H, W, r.cout);
+  gnorm(c, h1, nullptr, r.n2w, r.n2b, eps, 1, gn2);
+  drop(c, h1);
+  Act sc;
+  const void* res = x.p;
+  if (r.shortcut) {
+    sc = new_act(c, B, H, W, r.cout);
+    conv2d(c, x, nullptr, r.scw, r.scb, r.cout, 1, 1, 0, 0, H, W, sc);
+    res = sc.p;
+  }
+  Act out = new_act(c, B, H, W, r.cout);
+  conv2d(c, gn2, nullptr, r.c2w, r.c2b, r.cout, 3, 1, 1, 1, H, W, out, nullptr, 0, res);
+  drop(c, gn2);
+  if (r.shortcut) drop(c, sc);
+  return out;
+}
+
+// Mid-block single-head attention (d = 512): scores materialised per image (fp32), row softmax,
+// P V with V transposed once.  Batched MFMA GEMMs over the images.  The key axis is padded to a
+// multiple of 8 (zero probabilities / zero V^T columns) so the PV contraction stays 16-byte aligned.
+Act Vae::attn(Ctx& c, const AttW& a, Act& x) {
+  const int B = x.n, HW = x.h * x.w, C = a.c;
+  const int HWp = (HW + 7) / 8 * 8;
+  const long M = (long)B * HW;
+  const size_t es = dsize(dt_);
+  Act gn = new_act(c, B, x.h, x.w, C);
+  gnorm(c, x, nullptr, a.gw, a.gb, cfg_.norm_eps, 0, gn);
+  void* qkv = c.ws->alloc(M * 3 * C * es);
+  linear(c, gn.p, C, M, C, a.qkvw, 3 * C, fptr(a.qkvb), qkv, 3 * C);
+  drop(c, gn);
+  float* S = (float*)c.ws->alloc((size_t)B * HW * HWp * sizeof(float));
+  if (!c.ws->dry()) {
+    GemmArgs g;
+    g.dtype = dt_; g.M = HW; g.N = HW; g.K = C;
+    g.A = qkv; g.lda = 3 * C; g.sA = (long)HW * 3 * C;
+    g.B = (char*)qkv + C * es; g.ldb = 3 * C; g.sB = g.sA;
+    g.C = S; g.ldc = HWp; g.sC = (long)HW * HWp; g.out_f32 = 1;
+    g.alpha = 1.0f / std::sqrt((float)C);
+    g.batch = B;
+    gemm(g, c.s);
+  }
+  void* P = c.ws->alloc((size_t)B * HW * HWp * es);
+  if (!c.ws->dry()) softmax_rows(dt_, S, HWp, B * HW, HW, P, HWp, c.s);   // writes zeros in cols [HW, HWp)
+  c.ws->free(S);
+  void* VT = c.ws->alloc((size_t)B * C * HWp * es);
+  if (!c.ws->dry()) {
+    if (HWp != HW) IRX_HIP(hipMemsetAsync(VT, 0, (size_t)B * C * HWp * es, c.s));
+    transpose2d(dt_, (char*)qkv + 2 * C * es, 3 * C, HW, C, VT, HWp, B, (long)HW * 3 * C, (long)C * HWp, c.s);
+  }
+  c.ws->free(qkv);
+  void* O = c.ws->alloc(M * C * es);
+  if (!c.ws->dry()) {
+    GemmArgs g;
+    g.dtype = dt_; g.M = HW; g.N = C; g.K = HWp;
+    g.A = P; g.lda = HWp; g.sA = (long)HW * HWp;
+    g.B = VT; g.ldb = HWp; g.sB = (long)C * HWp;
+    g.C = O; g.ldc = C; g.sC = (long)HW * C;
+    g.batch = B;
+    gemm(g, c.s);
+  }
+  c.ws->free(P);
+  c.ws->free(VT);
+  Act out = new_act(c, B, x.h, x.w, C);
+  linear(c, O, C, M, C, a.ow, C, fptr(a.ob), out.p, C, ACT_NONE, x.p, C);
+  c.ws->free(O);
+  return out;
+}
+
+void Vae::run_encode(Ctx& c, const void* img, int B, int H, int W, void* moments) {
+  const int* bo = cfg_.block_out_channels;
+  const int nb = cfg_.n_blocks;
+  Act x;
+  x.p = const_cast<void*>(img); x.n = B; x.h = H; x.w = W; x.c = 8;
+  Act cur = new_act(c, B, H, W, bo[0]);
+  conv2d(c, x, nullptr, e_cin_w, e_cin_b, bo[0], 3, 1, 1, 1, H, W, cur);
+  for (int i = 0; i < nb; ++i) {
+    for (auto& r : e_res_[i]) {
+      Act nx = resnet(c, r, cur);
+      drop(c, cur);
+      cur = nx;
+    }
+    if (i < nb - 1) {
+      // Downsample2D(padding=0): F.pad(x, (0,1,0,1)) then 3x3 stride-2 conv
+      const int Ho = (cur.h + 1 - 3) / 2 + 1, Wo = (cur.w + 1 - 3) / 2 + 1;
+      Act d = new_act(c, B, Ho, Wo, cur.c);
+      conv2d(c, cur, nullptr, e_down_w_[i], e_down_b_[i], cur.c, 3, 2, 0, 0, cur.h, cur.w, d);
+      drop(c, cur);
+      cur = d;
+    }
+  }
+  Act r = resnet(c, e_mid0_, cur);
+  drop(c, cur);
+  Act a = attn(c, e_att_, r);
+  drop(c, r);
+  cur = resnet(c, e_mid1_, a);
+  drop(c, a);
+  Act gn = new_act(c, B, cur.h, cur.w, cur.c);
+  gnorm(c, cur, nullptr, e_nout_w, e_nout_b, cfg_.norm_eps, 1, gn);
+  drop(c, cur);
+  Act co = new_act(c, B, gn.h, gn.w, 8);
+  conv2d(c, gn, nullptr, e_cout_w, e_cout_b, 8, 3, 1, 1, 1, gn.h, gn.w, co);
+  drop(c, gn);
+  linear(c, co.p, 8, co.pix(), 8, qw, 8, fptr(qb), moments, 8);
+  drop(c, co);
+}
+
+void Vae::run_decode(Ctx& c, const void* z, int B, int h, int w, void* out) {
+  const int* bo = cfg_.block_out_channels;
+  const int nb = cfg_.n_blocks;
+  const int cm = bo[nb - 1];
+  Act zq = new_act(c, B, h, w, 8);
+  linear(c, z, 8, (long)B * h * w, 8, pqw, 8, fptr(pqb), zq.p, 8);
+  Act cur = new_act(c, B, h, w, cm);
+  conv2d(c, zq, nullptr, d_cin_w, d_cin_b, cm, 3, 1, 1, 1, h, w, cur);
+  drop(c, zq);
+  Act r = resnet(c, d_mid0_, cur);
+  drop(c, cur);
+  Act a = attn(c, d_att_, r);
+  drop(c, r);
+  cur = resnet(c, d_mid1_, a);
+  drop(c, a);
+  for (int i = 0; i < nb; ++i) {
+    for (auto& rr : d_res_[i]) {
+      Act nx = resnet(c, rr, cur);
+      drop(c, cur);
+      cur = nx;
+    }
+    if (i < nb - 1) {
+      Act u = new_act(c, B, cur.h * 2, cur.w * 2, cur.c);
+      conv2d(c, cur, nullptr, d_up_w_[i], d_up_b_[i], cur.c, 3, 1, 1, 1, cur.h * 2, cur.w * 2, u);
+      drop(c, cur);
+      cur = u;
+    }
+  }
+  Act gn = new_act(c, B, cur.h, cur.w, cur.c);
+  gnorm(c, cur, nullptr, d_nout_w, d_nout_b, cfg_.norm_eps, 1, gn);
+  drop(c, cur);
+  Act o;
+  o.p = out; o.n = B; o.h = gn.h; o.w = gn.w; o.c = 4;
+  conv2d(c, gn, nullptr, d_cout_w, d_cout_b, 4, 3, 1, 1, 1, gn.h, gn.w, o);
+  drop(c, gn);
+}
+
+size_t Vae::encode_ws(int B, int H, int W) {
+  Arena ar;
+  ar.reset(nullptr, 0);
+  Ctx c{nullptr, &ar};
+  run_encode(c, nullptr, B, H, W, nullptr);
+  return ar.peak();
+}
+size_t Vae::decode_ws(int B, int h, int w) {
+  Arena ar;
+  ar.reset(nullptr, 0);
+  Ctx c{nullptr, &ar};
+  run_decode(c, nullptr, B, h, w, nullptr);
+  return ar.peak();
+}
+void Vae::encode(hipStream_t s, const void* img, int B, int H, int W, void* moments, char* ws, size_t cap) {
+  IRX_CHECK(blob_, "weights not bound");
+  IRX_CHECK(H % 8 == 0 && W % 8 == 0, "VAE encode needs H, W multiples of 8");
+  Arena ar;
+  ar.reset(ws, cap);
+  Ctx c{s, &ar};
+  run_encode(c, img, B, H, W, moments);
+}
+void Vae::decode(hipStream_t s, const void* z, int B, int h, int w, void* out, char* ws, size_t cap) {
+  IRX_CHECK(blob_, "weights not bound");
+  Arena ar;
+  ar.reset(ws, cap);
+  Ctx c{s, &ar};
+  run_decode(c, z, B, h, w, out);
+}
+
+// ---------------------------------------------------------------------------------------------- CLIP
+Clip::Clip(const irx_model_config& cfg, int dtype) : Model(IRX_MODEL_CLIP, cfg, dtype) {
+  const int D = cfg.hidden_size, F = cfg.intermediate_size;
+  IRX_CHECK(D > 0 && F > 0 && cfg.num_layers > 0 && D % cfg.heads == 0, "bad CLIP config");
+  const std::string p = "text_model.";
+  tok = reg(p + "embeddings.token_embedding.weight", IRX_LAYOUT_EMB, dt_, {cfg.vocab_size, D});
+  pos = reg(p + "embeddings.position_embedding.weight", IRX_LAYOUT_EMB, dt_, {cfg.max_positions, D});
+  for (int i = 0; i < cfg.num_layers; ++i) {
+    const std::string b = p + "encoder.layers." + std::to_string(i) + ".";
+    const std::string s = b + "self_attn.";
+    Layer l;
+    l.ln1w = vec(b + "layer_norm1.weight", D); l.ln1b = vec(b + "layer_norm1.bias", D);
+    l.qkvw = mat(s + "q_proj.weight|" + s + "k_proj.weight|" + s + "v_proj.weight", 3 * D, D);
+    l.qkvb = vec(s + "q_proj.bias|" + s + "k_proj.bias|" + s + "v_proj.bias", 3 * D);
+    l.ow = mat(s + "out_proj.weight", D, D); l.ob = vec(s + "out_proj.bias", D);
+    l.ln2w = vec(b + "layer_norm2.weight", D); l.ln2b = vec(b + "layer_norm2.bias", D);
+    l.f1w = mat(b + "mlp.fc1.weight", F, D); l.f1b = vec(b + "mlp.fc1.bias", F);
+    l.f2w = mat(b + "mlp.fc2.weight", D, F); l.f2b = vec(b + "mlp.fc2.bias", D);
+    layers_.push_back(l);
+  }
+  fw = vec(p + "final_layer_norm.weight", D); fb = vec(p + "final_layer_norm.bias", D);
+}
+
+void Clip::run(Ctx& c, const int* ids, int B, int L, void* out) {
+  const int D = cfg_.hidden_size, F = cfg_.intermediate_size, H = cfg_.heads;
+  const long M = (long)B * L;
+  const size_t es = dsize(dt_);
+  const float eps = cfg_.layer_norm_eps;
+  void* h = c.ws->alloc(M * D * es);
+  void* n = c.ws->alloc(M * D * es);
+  void* qkv = c.ws->alloc(M * 3 * D * es);
+  void* att = c.ws->alloc(M * D * es);
+  void* f = c.ws->alloc(M * F * es);
+  if (!c.ws->dry()) embed_tokens(dt_, ids, B, L, ptr(tok), ptr(pos), D, h, c.s);
+  for (auto& l : layers_) {
+    lnorm(c, h, M, D, l.ln1w, l.ln1b, eps, n);
+    linear(c, n, D, M, D, l.qkvw, 3 * D, fptr(l.qkvb), qkv, 3 * D);
+    if (!c.ws->dry()) {
+      AttnArgs aa;
+      aa.dtype = dt_; aa.B = B; aa.H = H; aa.Lq = L; aa.Lk = L; aa.d = D / H;
+      aa.scale = 1.0f / std::sqrt((float)(D / H));
+      aa.causal = 1;
+      aa.q = qkv; aa.ldq = 3 * D; aa.sq = (long)L * 3 * D;
+      aa.k = (char*)qkv + D * es; aa.ldk = 3 * D; aa.sk = aa.sq;
+      aa.v = (char*)qkv + 2 * D * es; aa.ldv = 3 * D; aa.sv = aa.sq;
+      aa.o = att; aa.ldo = D; aa.so = (long)L * D;
+      attention(aa, c.s);
+    }
+    linear(c, att, D, M, D, l.ow, D, fptr(l.ob), h, D, ACT_NONE, h, D);
+    lnorm(c, h, M, D, l.ln2w, l.ln2b, eps, n);
+    linear(c, n, D, M, D, l.f1w, F, fptr(l.f1b), f, F, cfg_.quick_gelu ? ACT_QUICK_GELU : ACT_GELU);
+    linear(c, f, F, M, F, l.f2w, D, fptr(l.f2b), h, D, ACT_NONE, h, D);
+  }
+  lnorm(c, h, M, D, fw, fb, eps, out);
+  c.ws->free(f);
+  c.ws->free(att);
+  c.ws->free(qkv);
+  c.ws->free(n);
+  c.ws->free(h);
+}
+
+size_t Clip::workspace_bytes(int B, int L) {
+  Arena ar;
+  ar.reset(nullptr, 0);
+  Ctx c{nullptr, &ar};
+  run(c, nullptr, B, L, nullptr);
+  return ar.peak();
+}
+
+void Clip::encode(hipStream_t s, const int* ids, int B, int L, void* out, char* ws, size_t cap) {
+  IRX_CHECK(blob_, "weights not bound");
+  IRX_CHECK(L <= cfg_.max_positions, "prompt longer than max_position_embeddings");
+  Arena ar;
+  ar.reset(ws, cap);
+  Ctx c{s, &ar};
+  run(c, ids, B, L, out);
+}
+
+}  // namespace irx

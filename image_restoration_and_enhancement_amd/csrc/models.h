@@ -1,0 +1,172 @@
+// irx — native model graphs (UNet2DConditionModel, AutoencoderKL, CLIPTextModel) over the irx kernels.
+#pragma once
+#include <map>
+#include <memory>
+#include <vector>
+
+#include "../../include/irx.h"
+#include "ops.h"
+
+namespace irx {
+
+// Deterministic first-fit allocator over a caller-owned workspace.  Run once with base == nullptr
+// ("dry run": no kernels launched) to size the workspace, then for real with identical calls.
+class Arena {
+ public:
+  void reset(char* base, size_t cap) {
+    base_ = base; cap_ = cap; end_ = 0; peak_ = 0; free_.clear(); live_.clear();
+  }
+  void* alloc(size_t bytes);
+  void free(void* p);
+  size_t peak() const { return peak_; }
+  bool dry() const { return base_ == nullptr; }
+
+ private:
+  char* base_ = nullptr;
+  size_t cap_ = 0, end_ = 0, peak_ = 0;
+  std::map<size_t, size_t> free_;    // offset -> size of free holes below end_
+  std::map<size_t, size_t> live_;    // offset -> size
+};
+
+struct P { size_t off = 0; bool set = false; };   // parameter reference into the weight blob
+
+struct ParamEntry {
+  std::string name;
+  int layout, dtype;
+  std::vector<int64_t> shape;
+  size_t off, bytes;
+};
+
+struct Act {   // NHWC activation view
+  void* p = nullptr;
+  int n = 0, h = 0, w = 0, c = 0;
+  long pix() const { return (long)n * h * w; }
+};
+
+class Model {
+ public:
+  Model(int kind, const irx_model_config& cfg, int dtype) : kind_(kind), cfg_(cfg), dt_(dtype) {}
+  virtual ~Model() = default;
+  int kind() const { return kind_; }
+  int dtype() const { return dt_; }
+  const std::vector<ParamEntry>& manifest() const { return params_; }
+  size_t blob_bytes() const { return blob_bytes_; }
+  void bind(void* blob, size_t bytes);
+
+ protected:
+  P reg(const std::string& name, int layout, int dtype, std::vector<int64_t> shape);
+  P vec(const std::string& name, int64_t n) { return reg(name, IRX_LAYOUT_VEC, F32, {n}); }
+  P mat(const std::string& name, int64_t n, int64_t k) { return reg(name, IRX_LAYOUT_MAT, dt_, {n, k}); }
+  P conv(const std::string& name, int64_t co, int64_t kh, int64_t kw, int64_t ci) {
+    return reg(name, IRX_LAYOUT_CONV, dt_, {co, kh, kw, ci});
+  }
+  template <typename X = void> const X* ptr(P p) const { return (const X*)(blob_ + p.off); }
+  const float* fptr(P p) const { return (const float*)(blob_ + p.off); }
+
+  // ---- op helpers (skip launches in dry-run mode)
+  struct Ctx { hipStream_t s; Arena* ws; };
+  Act new_act(Ctx& c, int n, int h, int w, int ch);
+  void drop(Ctx& c, Act& a) { c.ws->free(a.p); a.p = nullptr; }
+  void conv2d(Ctx& c, const Act& x0, const Act* x1, P w, P b, int cout, int k, int stride, int pad_t, int pad_l,
+              int hv, int wv, const Act& out, const float* rowadd = nullptr, long rowadd_ld = 0,
+              const void* residual = nullptr, int out_f32 = 0, int ldc = -1);
+  void linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, const float* bias, void* C, long ldc,
+              int act = ACT_NONE, const void* residual = nullptr, long ldr = 0, int out_f32 = 0);
+  void gnorm(Ctx& c, const Act& x0, const Act* x1, P g, P b, float eps, int silu, const Act& out);
+  void lnorm(Ctx& c, const void* x, int rows, int C, P g, P b, float eps, void* out);
+
+  int kind_;
+  irx_model_config cfg_;
+  int dt_;
+  std::vector<ParamEntry> params_;
+  size_t blob_bytes_ = 0;
+  char* blob_ = nullptr;
+};
+
+// ------------------------------------------------------------------ shared blocks
+struct ResW {
+  P n1w, n1b, c1w, c1b, n2w, n2b, c2w, c2b, scw, scb;
+  int cin = 0, cout = 0;
+  bool shortcut = false;
+  long temb_off = -1;     // column offset into the fused time_emb_proj output (UNet only)
+};
+
+class Unet : public Model {
+ public:
+  Unet(const irx_model_config& cfg, int dtype);
+  int cin_pad() const { return cin_pad_; }
+  size_t workspace_bytes(int B, int h, int w);
+  size_t context_bytes(int B, int L) const { return (size_t)B * L * kv_cols_ * dsize(dt_); }
+  void prepare_context(hipStream_t s, const void* ctx, int B, int L, void* kv, char* ws, size_t cap);
+  void forward(hipStream_t s, const void* x, int B, int h, int w, const float* t, const void* kv, int L, float* eps,
+               char* ws, size_t cap);
+
+ private:
+  struct XfW {
+    P nw, nb, piw, pib, ln1w, ln1b, qkvw, o1w, o1b, ln2w, ln2b, q2w, o2w, o2b, ln3w, ln3b, ffw, ffb, ff2w, ff2b, pow,
+        pob;
+    int c = 0;
+    long kv_off = 0;      // column offset into the fused cross-attention K|V cache
+  };
+  struct Block {
+    std::vector<ResW> res;
+    std::vector<XfW> attn;
+    bool has_attn = false, resample = false;
+    P rsw, rsb;           // down/upsampler conv
+    int ch = 0;
+  };
+  ResW make_res(const std::string& p, int cin, int cout);
+  XfW make_xf(const std::string& p, int c);
+  void run(Ctx& c, const void* x, int B, int h, int w, const float* t, const void* kv, int L, float* eps);
+  Act resnet(Ctx& c, const ResW& r, Act& x0, Act* x1, const float* tproj, float eps);
+  Act transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L);
+
+  int cin_pad_ = 8;
+  int temb_dim_ = 1280;
+  long temb_cols_ = 0, kv_cols_ = 0;
+  std::vector<std::string> temb_names_w_, temb_names_b_, kv_names_;
+  P conv_in_w, conv_in_b, t1w, t1b, t2w, t2b, tpw, tpb, kvw, nout_w, nout_b, conv_out_w, conv_out_b;
+  std::vector<Block> down_, up_;
+  ResW mid_res0_, mid_res1_;
+  XfW mid_attn_;
+};
+
+class Vae : public Model {
+ public:
+  Vae(const irx_model_config& cfg, int dtype);
+  size_t encode_ws(int B, int H, int W);
+  size_t decode_ws(int B, int h, int w);
+  void encode(hipStream_t s, const void* img, int B, int H, int W, void* moments, char* ws, size_t cap);
+  void decode(hipStream_t s, const void* z, int B, int h, int w, void* out, char* ws, size_t cap);
+
+ private:
+  struct AttW { P gw, gb, qkvw, qkvb, ow, ob; int c = 0; };
+  ResW make_res(const std::string& p, int cin, int cout);
+  AttW make_attn(const std::string& p, int c);
+  Act resnet(Ctx& c, const ResW& r, Act& x);
+  Act attn(Ctx& c, const AttW& a, Act& x);
+  void run_encode(Ctx& c, const void* img, int B, int H, int W, void* moments);
+  void run_decode(Ctx& c, const void* z, int B, int h, int w, void* out);
+
+  P e_cin_w, e_cin_b, e_nout_w, e_nout_b, e_cout_w, e_cout_b, qw, qb, pqw, pqb, d_cin_w, d_cin_b, d_nout_w,
+      d_nout_b, d_cout_w, d_cout_b;
+  std::vector<std::vector<ResW>> e_res_, d_res_;
+  std::vector<P> e_down_w_, e_down_b_, d_up_w_, d_up_b_;
+  ResW e_mid0_, e_mid1_, d_mid0_, d_mid1_;
+  AttW e_att_, d_att_;
+};
+
+class Clip : public Model {
+ public:
+  Clip(const irx_model_config& cfg, int dtype);
+  size_t workspace_bytes(int B, int L);
+  void encode(hipStream_t s, const int* ids, int B, int L, void* out, char* ws, size_t cap);
+
+ private:
+  struct Layer { P ln1w, ln1b, qkvw, qkvb, ow, ob, ln2w, ln2b, f1w, f1b, f2w, f2b; };
+  void run(Ctx& c, const int* ids, int B, int L, void* out);
+  P tok, pos, fw, fb;
+  std::vector<Layer> layers_;
+};
+
+}  // namespace irx

@@ -1,0 +1,116 @@
+// irx — host-side launchers for the hand-written gfx950 kernels.
+// Every activation is NHWC ([N][H][W][C], C fastest); weights are [Cout][KH][KW][Cin] (K-contiguous).
+#pragma once
+#include "irx_common.h"
+
+namespace irx {
+
+// ------------------------------------------------------------ implicit-GEMM convolution / GEMM
+// A operand either a dense row-major matrix or an NHWC image gathered on the fly (3x3 / 1x1 convs,
+// stride 1/2, asymmetric zero padding, fused nearest-neighbour upsample, fused channel concat of two
+// sources).  B = weights [N][K] with K contiguous.  C[m][n] = epilogue(sum_k A[m][k] B[n][k]).
+struct ConvGeom {
+  const void* src0 = nullptr;   // NHWC, C0 channels
+  const void* src1 = nullptr;   // optional second NHWC source (channel concat), C1 channels
+  int C0 = 0, C1 = 0;
+  int N = 0, Hin = 0, Win = 0;  // stored input size
+  int Hv = 0, Wv = 0;           // virtual input size after nearest resize (== Hin/Win if none)
+  int KH = 1, KW = 1, stride = 1, pad_t = 0, pad_l = 0;
+  int Ho = 0, Wo = 0;
+};
+
+struct GemmArgs {
+  int dtype = BF16;       // storage type of A, B, residual and (unless out_f32) C
+  int M = 0, N = 0, K = 0;
+  int conv = 0;           // 1: A is an implicit im2col of `g`
+  ConvGeom g;
+  const void* A = nullptr; long lda = 0; long sA = 0;    // dense A (+ batch stride)
+  const void* B = nullptr; long ldb = 0; long sB = 0;
+  void* C = nullptr; long ldc = 0; long sC = 0;
+  int out_f32 = 0;        // C stored as fp32 regardless of dtype
+  float alpha = 1.f;
+  const float* bias = nullptr;                  // [N]
+  const float* rowadd = nullptr; long rowadd_ld = 0; int rows_per_group = 1;  // += rowadd[(m/rpg)*ld + n]
+  const void* residual = nullptr; long ldr = 0; long sR = 0;                  // += residual[m][n] (dtype)
+  float out_scale = 1.f;
+  int act = ACT_NONE;     // applied after bias/rowadd, before residual
+  int batch = 1;
+};
+void gemm(const GemmArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------ normalisation
+// GroupNorm over NHWC (optionally a channel concat of two sources). Writes the normalised (and
+// optionally SiLU'd) result as one contiguous C0+C1 channel tensor.  `ws` needs gn_ws_bytes().
+size_t gn_ws_bytes(int N, int HW, int G);
+void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
+                const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s);
+void layer_norm(int dtype, const void* x, long ldx, int rows, int C, float eps, const float* gamma,
+                const float* beta, void* out, long ldo, hipStream_t s);
+
+// ------------------------------------------------------------ attention
+// Multi-head attention, flash-style (online softmax, never materialises scores).
+// q[b][i][h*d + e] with row stride ldq (elements), batch stride sq; likewise k, v, o.
+struct AttnArgs {
+  int dtype = BF16;
+  int B = 1, H = 1, Lq = 0, Lk = 0, d = 0;
+  const void* q = nullptr; long ldq = 0, sq = 0;
+  const void* k = nullptr; long ldk = 0, sk = 0;
+  const void* v = nullptr; long ldv = 0, sv = 0;
+  void* o = nullptr; long ldo = 0, so = 0;
+  float scale = 1.f;
+  int causal = 0;
+};
+void attention(const AttnArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------ elementwise / data movement
+void geglu(int dtype, const void* proj, long ldp, int M, int F, void* out, long ldo, hipStream_t s);
+void timestep_embed(int dtype, const float* t, int B, int dim, int flip_sin_to_cos, float shift, void* out,
+                    hipStream_t s);
+void embed_tokens(int dtype, const int* ids, int B, int L, const void* tok, const void* pos, int D, void* out,
+                  hipStream_t s);
+void transpose2d(int dtype, const void* in, long ldi, int rows, int cols, void* out, long ldo, int batch,
+                 long s_in, long s_out, hipStream_t s);
+void softmax_rows(int dtype, const float* in, long ldi, int rows, int cols, void* out, long ldo, hipStream_t s);
+
+// image uint8 NHWC (3 ch) -> [-1,1] dtype NHWC with `cpad` channels (zero padded); optional mask [N][H][W]
+// (1 = inpaint) zeroes masked pixels: init_image * (mask < 0.5)
+void image_to_tensor(int dtype, const uint8_t* img, const float* mask, int N, int H, int W, int cpad, void* out,
+                     hipStream_t s);
+// decoded dtype NHWC (ldc channels, first 3 used) -> uint8 (+ optional fp32 [0,1] copy)
+void tensor_to_image(int dtype, const void* x, int N, int H, int W, int ldc, uint8_t* img, float* f01,
+                     hipStream_t s);
+// moments [N][h][w][mcs] (mean = ch 0..3, logvar = ch 4..7) -> z = (mean + exp(.5*clamp(logvar))*eps)*sf,
+// then optionally x = a*z + b*noise.  eps/noise fp32 [N][h][w][4] (or broadcast over N if bcast).
+void latent_sample(int dtype, const void* moments, int mcs, int N, int h, int w, const float* eps,
+                   const float* noise, int bcast, float sf, float a, float b, float* out, hipStream_t s);
+
+// Fused classifier-free-guidance + scheduler update + next-step UNet input packing.
+struct StepArgs {
+  int dtype = BF16;
+  int B = 1, h = 0, w = 0;               // latent batch (images), spatial size
+  const float* eps = nullptr;            // UNet output fp32 [(cfg?2B:B)][h][w][4]
+  int cfg = 0; float guidance = 1.f;
+  // history ring (PNDM): store the CFG-combined eps into hist_store (may be null)
+  float* hist_store = nullptr;
+  const float* hist[4] = {nullptr, nullptr, nullptr, nullptr};   // previous eps entries
+  float hw[5] = {1.f, 0.f, 0.f, 0.f, 0.f};  // e = (hw0*eps + hw1*h0 + hw2*h1 + hw3*h2 + hw4*h3)*e_scale
+  float e_div = 1.f;                        // e /= e_div  (applied after the weighted sum)
+  float e_mul = 1.f;                        // e *= e_mul  (PNDM 4th-order form multiplies by 1/24)
+  int mode = 0;                             // 0 = PNDM _get_prev_sample, 1 = DDIM
+  float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;   // scalar coefficients (see kernel)
+  const float* x_src = nullptr;             // sample the update applies to
+  float* cur_store = nullptr;               // PNDM: keep a copy of x_src (cur_sample)
+  float* x_out = nullptr;                   // new latents fp32 [B][h][w][4]
+  // next UNet input (dtype) [(cfg?2B:B)][h][w][cin_pad]: latents, then (inpaint) mask + masked latents
+  void* unet_in = nullptr; int cin_pad = 8; int inpaint = 0;
+  const float* mask = nullptr;              // [B][h][w] (inpaint)
+  const float* masked = nullptr;            // [B][h][w][4] (inpaint)
+};
+void sched_step(const StepArgs& a, hipStream_t s);
+// pack fp32 latents into the UNet input layout (same packing as sched_step's tail)
+void pack_unet_input(int dtype, const float* lat, int B, int h, int w, int cfg, int cin_pad, int inpaint,
+                     const float* mask, const float* masked, void* out, hipStream_t s);
+void scale_copy(int dtype_out, const float* in, long n, float scale, void* out, int in_ch, int out_ch,
+                hipStream_t s);
+
+}  // namespace irx

@@ -1,0 +1,248 @@
+"""Batched SD-1.5 img2img / inpaint orchestration over the native engine.
+
+Restates the control flow of diffusers 0.35.2 `StableDiffusionImg2ImgPipeline.__call__` and
+`StableDiffusionInpaintPipeline.__call__` — the calls the reference
+makes at `src/inference.py:486-495, :566-573, :664-672, :758-767` — for a batch of images that
+share a prompt.  Everything between the uint8 input pixels and the uint8 output pixels runs on the
+GPU through libirx: pixel normalisation, VAE encode, posterior sampling + add_noise, CLIP text
+encoding, the denoising loop (UNet + fused CFG/scheduler/pack step kernel), VAE decode and the
+uint8 post-processing.  The host only resizes with PIL, draws the seeded noise (CPU
+`torch.Generator`, exactly like the reference on a CPU device) and plans scheduler coefficients.
+
+Every image gets the noise of a fresh `Generator.manual_seed(seed)`, because the reference
+reseeds per call (`src/inference.py:482-483, :562-563, :660-661, :754-755`) and calls the
+pipeline once per image.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import image_processor as ip
+from . import weights as W
+from .configs import PipelineConfig
+from .engine import CLIPText, UNet, VAE, TORCH_DT, dtype_code
+from .schedulers import make_planner, StepPlan
+from .tokenizer import PromptTokenizer
+
+
+@dataclass
+class BatchResult:
+    images_u8: torch.Tensor                 # [B, H, W, 3] uint8 (device)
+    decoded01: Optional[torch.Tensor]       # [B, H, W, 3] fp32 in [0, 1] before rounding (device) or None
+    latents: torch.Tensor                   # [B, h, w, 4] fp32 final latents (device)
+    timesteps: List[int]
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def draw_noise(seed: int, h: int, w: int, n: int) -> List[torch.Tensor]:
+    """The reference's RNG draws for one image: n x randn(1, 4, h, w) from Generator('cpu').manual_seed(seed),
+    returned as NHWC [h, w, 4] fp32 (CPU)."""
+    g = torch.Generator("cpu").manual_seed(seed)
+    out = []
+    for _ in range(n):
+        e = torch.randn((1, 4, h, w), generator=g, dtype=torch.float32)
+        out.append(e[0].permute(1, 2, 0).contiguous())
+    return out
+
+
+class SDEngine:
+    """The three native models of one task directory + the batched denoising loop."""
+
+    def __init__(self, cfg: PipelineConfig, dtype="bf16", device="cuda", weights="random", weight_seed: int = 0,
+                 state_dicts: Optional[Dict[str, Dict[str, torch.Tensor]]] = None):
+        self.cfg = cfg
+        self.dt = dtype_code(dtype)
+        self.tdt = TORCH_DT[self.dt]
+        self.device = torch.device(device)
+        self.unet = UNet(cfg.unet, self.dt, self.device)
+        self.vae = VAE(cfg.vae, self.dt, self.device)
+        self.clip = CLIPText(cfg.clip, self.dt, self.device)
+        if state_dicts is None:
+            state_dicts = self._load_weights(weights, weight_seed)
+        if state_dicts is not None:
+            self.unet.load_state_dict(state_dicts["unet"])
+            self.vae.load_state_dict(state_dicts["vae"])
+            self.clip.load_state_dict(state_dicts["clip"])
+        tok_dir = Path(cfg.model_dir) / "tokenizer" if cfg.model_dir else None
+        self.tokenizer = PromptTokenizer(tok_dir)
+        self._ctx_cache: Dict[tuple, torch.Tensor] = {}
+
+    # ------------------------------------------------------------------ weights
+    def _load_weights(self, weights, seed):
+        if weights == "none":
+            return None          # caller binds blobs itself (e.g. after an RCCL broadcast)
+        if weights == "random":
+            return {k: W.random_state_dict(k, getattr(self.cfg, k), seed) for k in ("unet", "vae", "clip")}
+        root = Path(weights if weights != "dir" else self.cfg.model_dir)
+        sds = {"unet": W.load_component_dir(root / "unet"), "vae": W.load_component_dir(root / "vae"),
+               "clip": W.load_component_dir(root / "text_encoder")}
+        for k in sds:
+            W.check_state_dict(k, getattr(self.cfg, k), sds[k])
+        return sds
+
+    def models(self):
+        return {"unet": self.unet, "vae": self.vae, "clip": self.clip}
+
+    # ------------------------------------------------------------------ text
+    def text_embeddings(self, prompt: str, cfg_on: bool, negative: str = "") -> torch.Tensor:
+        """encode_prompt: [neg, pos] (CFG) or [pos] -> [n, 77, 768] (dtype, device)."""
+        key = (prompt, negative, cfg_on)
+        if key not in self._ctx_cache:
+            ids = [self.tokenizer(negative), self.tokenizer(prompt)] if cfg_on else [self.tokenizer(prompt)]
+            ids = torch.from_numpy(np.stack(ids))
+            self._ctx_cache[key] = self.clip.encode(ids)
+        return self._ctx_cache[key]
+
+    def context_kv(self, emb: torch.Tensor, batch: int) -> torch.Tensor:
+        """UNet batch rows are [uncond x B, cond x B] (CFG) -> per-row cross-attention K|V."""
+        ctx = emb.repeat_interleave(batch, dim=0).contiguous()
+        return self.unet.prepare_context(ctx)
+
+    # ------------------------------------------------------------------ building blocks
+    def to_tensor(self, u8: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        B, H, W_, _ = u8.shape
+        out = torch.empty((B, H, W_, 8), dtype=self.tdt, device=self.device)
+        L.call("irx_image_to_tensor", _stream(), self.dt, _p(u8), _p(mask), B, H, W_, 8, _p(out))
+        return out
+
+    def sample_latents(self, moments: torch.Tensor, eps: torch.Tensor, noise: Optional[torch.Tensor],
+                       a: float = 1.0, b: float = 0.0) -> torch.Tensor:
+        B, h, w, _ = moments.shape
+        out = torch.empty((B, h, w, 4), dtype=torch.float32, device=self.device)
+        L.call("irx_latent_sample", _stream(), self.dt, _p(moments), B, h, w, _p(eps), _p(noise), 1,
+               float(self.cfg.vae.scaling_factor), float(a), float(b), _p(out))
+        return out
+
+    def decode(self, lat: torch.Tensor, want_float: bool) -> tuple:
+        B, h, w, _ = lat.shape
+        z = torch.empty((B, h, w, 8), dtype=self.tdt, device=self.device)
+        L.call("irx_latents_to_vae", _stream(), self.dt, _p(lat), B, h, w, float(self.cfg.vae.scaling_factor), _p(z))
+        img = self.vae.decode(z)
+        H, W_ = h * 8, w * 8
+        u8 = torch.empty((B, H, W_, 3), dtype=torch.uint8, device=self.device)
+        f01 = torch.empty((B, H, W_, 3), dtype=torch.float32, device=self.device) if want_float else None
+        L.call("irx_tensor_to_image", _stream(), self.dt, _p(img), B, H, W_, 4, _p(u8), _p(f01))
+        return u8, f01
+
+    def denoise_loop(self, lat: torch.Tensor, kv: torch.Tensor, plans: List[StepPlan], guidance: float,
+                     cfg_on: bool, mask_l: Optional[torch.Tensor] = None,
+                     masked_l: Optional[torch.Tensor] = None) -> torch.Tensor:
+        B, h, w, _ = lat.shape
+        UB = 2 * B if cfg_on else B
+        inpaint = int(mask_l is not None)
+        cp = self.unet.cin_pad
+        x_in = torch.empty((UB, h, w, cp), dtype=self.tdt, device=self.device)
+        L.call("irx_pack_unet_input", _stream(), self.dt, _p(lat), B, h, w, int(cfg_on), cp, inpaint, _p(mask_l),
+               _p(masked_l), _p(x_in))
+        eps = torch.empty((UB, h, w, 4), dtype=torch.float32, device=self.device)
+        n_slots = max([(-1 if p.store_slot is None else p.store_slot) for p in plans] + [-1]) + 1
+        slots = [torch.empty_like(lat) for _ in range(n_slots)]
+        cur = torch.empty_like(lat) if any(p.save_cur for p in plans) else None
+        t_all = torch.tensor([[float(p.t)] * UB for p in plans], dtype=torch.float32).to(self.device)
+        for i, p in enumerate(plans):
+            self.unet.forward(x_in, t_all[i], kv, 77, out=eps)
+            sp = L.StepParams()
+            sp.dtype, sp.batch, sp.h, sp.w = self.dt, B, h, w
+            sp.eps, sp.cfg, sp.guidance = eps.data_ptr(), int(cfg_on), float(guidance)
+            sp.hist_store = slots[p.store_slot].data_ptr() if p.store_slot is not None else None
+            for k in range(4):
+                sp.hist[k] = slots[p.hist[k]].data_ptr() if p.hist[k] is not None else None
+            for k in range(5):
+                sp.hw[k] = float(p.hw[k])
+            sp.e_div, sp.e_mul = float(p.e_div), float(p.e_mul)
+            sp.mode = p.mode
+            sp.c0, sp.c1, sp.c2, sp.c3 = (float(v) for v in p.c)
+            sp.x_src = (cur if p.x_from_cur else lat).data_ptr()
+            sp.cur_store = cur.data_ptr() if p.save_cur else None
+            sp.x_out = lat.data_ptr()
+            last = i + 1 == len(plans)
+            sp.unet_in = None if last else x_in.data_ptr()
+            sp.cin_pad, sp.inpaint = cp, inpaint
+            sp.mask, sp.masked = (mask_l.data_ptr() if inpaint else None), (masked_l.data_ptr() if inpaint else None)
+            L.call("irx_sched_step", _stream(), C.byref(sp))
+        return lat
+
+    # ------------------------------------------------------------------ pipelines
+    def img2img(self, u8: torch.Tensor, prompt: str, strength: float, steps: int, guidance: float, seed: int = 42,
+                want_float: bool = False, n_evals: Optional[int] = None,
+                noise: Optional[Sequence[torch.Tensor]] = None) -> BatchResult:
+        """u8: device uint8 [B, H, W, 3], H and W multiples of 8 (already preprocessed)."""
+        if not 0 <= strength <= 1:
+            raise ValueError(f"The value of strength should in [0.0, 1.0] but is {strength}")
+        if prompt is None:
+            raise ValueError("Provide either `prompt` or `prompt_embeds`.")
+        B, H, W_, _ = u8.shape
+        h, w = H // 8, W_ // 8
+        cfg_on = guidance > 1.0
+        planner = make_planner(self.cfg.scheduler)
+        planner.set_timesteps(steps)
+        ts, _ = planner.get_timesteps(steps, strength)
+        if len(ts) == 0:
+            raise ValueError("strength too small: no denoising steps")
+        plans = planner.plan(ts)
+        if n_evals is not None:
+            plans = plans[:n_evals]
+        emb = self.text_embeddings(prompt, cfg_on)
+        kv = self.context_kv(emb, B)
+        if noise is None:
+            noise = draw_noise(seed, h, w, 2)
+        eps1, nz = (x.to(self.device) for x in noise[:2])
+        img = self.to_tensor(u8)
+        mom = self.vae.encode(img)
+        a, b = planner.add_noise_coeffs(int(ts[0]))
+        lat = self.sample_latents(mom, eps1, nz, a, b)
+        lat = self.denoise_loop(lat, kv, plans, guidance, cfg_on)
+        u8o, f01 = self.decode(lat, want_float)
+        return BatchResult(u8o, f01, lat, [p.t for p in plans])
+
+    def inpaint(self, u8: torch.Tensor, mask01: torch.Tensor, prompt: str, strength: float, steps: int,
+                guidance: float, seed: int = 42, want_float: bool = False,
+                n_evals: Optional[int] = None) -> BatchResult:
+        """u8: device uint8 [B, H, W, 3] at the processor size; mask01: fp32 [B, H, W] of {0,1} (1 = inpaint)."""
+        B, H, W_, _ = u8.shape
+        h, w = H // 8, W_ // 8
+        cfg_on = guidance > 1.0
+        planner = make_planner(self.cfg.scheduler)
+        planner.set_timesteps(steps)
+        ts, n = planner.get_timesteps(steps, strength)
+        if n < 1:
+            raise ValueError("strength too small: no denoising steps")
+        plans = planner.plan(ts)
+        if n_evals is not None:
+            plans = plans[:n_evals]
+        emb = self.text_embeddings(prompt, cfg_on)
+        kv = self.context_kv(emb, B)
+        is_max = strength == 1.0
+        draws = draw_noise(seed, h, w, 2 if is_max else 3)
+        draws = [d.to(self.device) for d in draws]
+        img = self.to_tensor(u8)
+        if is_max:
+            nz, e3 = draws
+            # latents = noise * init_noise_sigma (1.0): a z-free sample (moments unused -> pass zeros)
+            lat = nz.unsqueeze(0).expand(B, h, w, 4).contiguous()
+        else:
+            e1, nz, e3 = draws
+            mom = self.vae.encode(img)
+            a, b = planner.add_noise_coeffs(int(ts[0]))
+            lat = self.sample_latents(mom, e1, nz, a, b)
+        masked_img = self.to_tensor(u8, mask01.contiguous())
+        mom2 = self.vae.encode(masked_img)
+        masked_l = self.sample_latents(mom2, e3, None)
+        mask_l = torch.from_numpy(ip.nearest_downsample(mask01.cpu().numpy(), h, w)).to(self.device).contiguous()
+        lat = self.denoise_loop(lat, kv, plans, guidance, cfg_on, mask_l, masked_l)
+        u8o, f01 = self.decode(lat, want_float)
+        return BatchResult(u8o, f01, lat, [p.t for p in plans])

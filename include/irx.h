@@ -1,0 +1,153 @@
+/* irx — MI355X-native Stable Diffusion restoration engine: public C ABI.
+ *
+ * The reference has no native interface: `src/inference.py` (RestorationPipeline,
+ * src/inference.py:48-890) calls diffusers pipelines whose components are the boundary this
+ * library replaces.  Each entry point below names the reference-side call it stands in for.
+ * Conventions:
+ *   - every function returns 0 on success, non-zero on failure; irx_last_error() gives a
+ *     thread-local message (reference error behaviour: the Python layer logs it and falls back,
+ *     src/inference.py:496-498, :575-577, :679-681, :774-776);
+ *   - tensors are raw DEVICE pointers owned by the caller (PyTorch-ROCm tensors used as
+ *     containers); the library never allocates or frees caller memory;
+ *   - activations are NHWC; `dtype` is IRX_F32 (parity mode) or IRX_BF16 (throughput mode);
+ *   - `stream` is a hipStream_t passed as void*; work is enqueued, nothing synchronises;
+ *   - a model handle is not thread-safe; use one handle per stream.
+ */
+#ifndef IRX_H_
+#define IRX_H_
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IRX_F32 0
+#define IRX_BF16 1
+
+#define IRX_MODEL_UNET 0
+#define IRX_MODEL_VAE 1
+#define IRX_MODEL_CLIP 2
+
+/* weight layouts of manifest entries (how the host packs diffusers tensors into the blob) */
+#define IRX_LAYOUT_VEC 0   /* [n] fp32, zero padded                                  */
+#define IRX_LAYOUT_MAT 1   /* [N][K] from [N][K] or [N][K][1][1], zero padded         */
+#define IRX_LAYOUT_CONV 2  /* [Cout][KH][KW][Cin] from OIHW, zero padded on Cout/Cin   */
+#define IRX_LAYOUT_EMB 3   /* [rows][D] embedding table                                */
+
+typedef struct irx_model irx_model;
+
+typedef struct {
+  /* UNet2DConditionModel (unet/config.json) / AutoencoderKL (vae/config.json) */
+  int in_channels, out_channels, latent_channels;
+  int n_blocks;
+  int block_out_channels[8];
+  int layers_per_block;
+  int heads;                /* UNet: "attention_head_dim" (= head count in SD-1.5) */
+  int cross_attention_dim;
+  int norm_groups;
+  float norm_eps;
+  int flip_sin_to_cos;
+  float freq_shift;
+  int down_attn[8], up_attn[8];
+  /* CLIPTextModel (text_encoder/config.json) */
+  int vocab_size, hidden_size, intermediate_size, num_layers, max_positions;
+  float layer_norm_eps;
+  int quick_gelu;
+} irx_model_config;
+
+typedef struct {
+  const char* name;   /* diffusers/transformers parameter name(s); '|' joins tensors concatenated on dim 0 */
+  int layout;         /* IRX_LAYOUT_* */
+  int dtype;          /* IRX_F32 or IRX_BF16 storage in the blob */
+  int ndim;
+  int64_t shape[4];   /* engine shape (padded) */
+  size_t offset;      /* byte offset in the weight blob */
+  size_t bytes;
+} irx_param_info;
+
+const char* irx_last_error(void);
+int irx_version(void);
+
+/* ---- model lifetime: replaces diffusers/transformers from_pretrained (src/inference.py:162-172) ---- */
+int irx_model_create(int kind, const irx_model_config* cfg, int dtype, irx_model** out);
+int irx_model_destroy(irx_model* m);
+int irx_model_num_params(const irx_model* m, int* n);
+int irx_model_param_info(const irx_model* m, int i, irx_param_info* info);
+int irx_model_blob_bytes(const irx_model* m, size_t* bytes);
+/* bind a device blob packed per the manifest (after upload or RCCL broadcast) */
+int irx_model_bind(irx_model* m, void* device_blob, size_t bytes);
+
+/* ---- UNet2DConditionModel.forward (diffusers; called per step at src/inference.py:486/:566/:664/:758) ---- */
+int irx_unet_workspace_bytes(const irx_model* m, int batch, int h, int w, size_t* bytes);
+int irx_unet_context_bytes(const irx_model* m, int batch, int ctx_len, size_t* bytes);
+/* cross-attention K/V of all transformer blocks for a fixed text context (computed once per call) */
+int irx_unet_prepare_context(irx_model* m, void* stream, const void* ctx, int batch, int ctx_len, void* ctx_kv,
+                             void* ws, size_t ws_bytes);
+/* x: [batch][h][w][cin_pad] dtype; t: device fp32 [batch]; eps_out: fp32 [batch][h][w][out_channels] */
+int irx_unet_forward(irx_model* m, void* stream, const void* x, int batch, int h, int w, const float* t,
+                     const void* ctx_kv, int ctx_len, float* eps_out, void* ws, size_t ws_bytes);
+int irx_unet_input_channels(const irx_model* m, int* cin_pad);
+
+/* ---- AutoencoderKL.encode / .decode (diffusers; img2img prepare_latents / final decode) ---- */
+int irx_vae_encode_workspace_bytes(const irx_model* m, int batch, int H, int W, size_t* bytes);
+/* img: [batch][H][W][8] dtype in [-1,1]; moments: [batch][H/8][W/8][8] dtype (mean 0..3, logvar 4..7) */
+int irx_vae_encode(irx_model* m, void* stream, const void* img, int batch, int H, int W, void* moments, void* ws,
+                   size_t ws_bytes);
+int irx_vae_decode_workspace_bytes(const irx_model* m, int batch, int h, int w, size_t* bytes);
+/* z: [batch][h][w][8] dtype (latents / scaling_factor, channels 4..7 zero); out: [batch][8h][8w][4] dtype */
+int irx_vae_decode(irx_model* m, void* stream, const void* z, int batch, int h, int w, void* out, void* ws,
+                   size_t ws_bytes);
+
+/* ---- CLIPTextModel.last_hidden_state (transformers; encode_prompt) ---- */
+int irx_clip_workspace_bytes(const irx_model* m, int batch, int len, size_t* bytes);
+/* ids: device int32 [batch][len]; out: [batch][len][hidden] dtype */
+int irx_clip_encode(irx_model* m, void* stream, const int* ids, int batch, int len, void* out, void* ws,
+                    size_t ws_bytes);
+
+/* ---- scheduler / pipeline glue (PNDMScheduler.step_plms, DDIMScheduler.step, CFG combine, add_noise,
+ *      DiagonalGaussianDistribution.sample, VaeImageProcessor pre/post) ---- */
+typedef struct {
+  int dtype;
+  int batch, h, w;
+  const float* eps; int cfg; float guidance;
+  float* hist_store; const float* hist[4]; float hw[5]; float e_div; float e_mul;
+  int mode; float c0, c1, c2, c3;
+  const float* x_src; float* cur_store; float* x_out;
+  void* unet_in; int cin_pad; int inpaint; const float* mask; const float* masked;
+} irx_step_params;
+int irx_sched_step(void* stream, const irx_step_params* p);
+int irx_pack_unet_input(void* stream, int dtype, const float* lat, int batch, int h, int w, int cfg, int cin_pad,
+                        int inpaint, const float* mask, const float* masked, void* out);
+int irx_latent_sample(void* stream, int dtype, const void* moments, int batch, int h, int w, const float* eps,
+                      const float* noise, int bcast, float scaling_factor, float a, float b, float* out);
+int irx_latents_to_vae(void* stream, int dtype, const float* lat, int batch, int h, int w, float scaling_factor,
+                       void* z);
+/* mask (nullable): fp32 [batch][H][W], 1 = region to inpaint; masked pixels become 0 (init_image * (mask < 0.5)) */
+int irx_image_to_tensor(void* stream, int dtype, const uint8_t* img, const float* mask, int batch, int H, int W,
+                        int cpad, void* out);
+int irx_tensor_to_image(void* stream, int dtype, const void* x, int batch, int H, int W, int ldc, uint8_t* img,
+                        float* f01);
+
+/* ---- single-op entry points (parity tests, composition) ---- */
+int irx_op_conv2d(void* stream, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hin, int win,
+                  int hv, int wv, const void* weight, const float* bias, int cout, int kh, int kw, int stride,
+                  int pad_t, int pad_l, int ho, int wo, const float* rowadd, long rowadd_ld, const void* residual,
+                  void* out, int out_f32, int act);
+int irx_op_gemm(void* stream, int dtype, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                void* C, long ldc, const float* bias, float alpha, int act, const void* residual, long ldr,
+                int out_f32, int batch, long sA, long sB, long sC, long sR);
+int irx_op_group_norm(void* stream, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hw,
+                      int groups, float eps, const float* gamma, const float* beta, int silu, void* out, void* ws);
+size_t irx_op_group_norm_ws_bytes(int n, int hw, int groups);
+int irx_op_layer_norm(void* stream, int dtype, const void* x, int rows, int c, float eps, const float* gamma,
+                      const float* beta, void* out);
+int irx_op_attention(void* stream, int dtype, int batch, int heads, int lq, int lk, int d, const void* q, long ldq,
+                     long sq, const void* k, long ldk, long sk, const void* v, long ldv, long sv, void* o, long ldo,
+                     long so, float scale, int causal);
+int irx_op_geglu(void* stream, int dtype, const void* proj, int M, int F, void* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IRX_H_ */

@@ -1,0 +1,208 @@
+"""GPU parity of every hand-written kernel (through the C ABI) against fp32 PyTorch-CPU references.
+
+Tolerances (max |err| / max |ref|): fp32 path 1e-4 (exact-f32 MFMA / fp32 VALU, different
+summation order only); bf16 path 2e-2 (bf16 storage of inputs/outputs, fp32 accumulation) with
+the reference fed the same bf16-rounded inputs.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tests import opref as O
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2}
+DTS = [torch.float32, torch.bfloat16]
+
+
+def _r(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+def _dev(x, dt, device):
+    return x.to(dt).to(device).contiguous()
+
+
+def _q(x, dt):      # what the device sees, back in fp32 for the CPU reference
+    return x.to(dt).float()
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("case", [
+    # (N, H, W, Cin, Cout, k, stride, pad)
+    (2, 16, 16, 64, 64, 3, 1, 1),
+    (1, 13, 9, 32, 40, 3, 1, 1),       # ragged spatial + N not a tile multiple
+    (2, 17, 12, 64, 64, 3, 2, 1),      # UNet Downsample2D on odd size
+    (1, 8, 8, 8, 320, 3, 1, 1),        # conv_in (4 channels padded to 8)
+    (2, 8, 8, 320, 4, 3, 1, 1),        # conv_out (N = 4)
+    (1, 12, 12, 96, 48, 1, 1, 0),      # 1x1 shortcut
+    (1, 40, 24, 128, 256, 3, 1, 1),
+])
+def test_conv(device, dt, case):
+    N, H, W, Ci, Co, k, s, p = case
+    x = _r(N, Ci, H, W, seed=1)
+    w = _r(Co, Ci, k, k, seed=2, scale=1 / math.sqrt(Ci * k * k))
+    b = _r(Co, seed=3)
+    got = O.conv2d(_dev(x.permute(0, 2, 3, 1), dt, device), w.to(dt).float(), b, stride=s, pad=(p, p))
+    ref = F.conv2d(_q(x, dt), _q(w, dt), b, stride=s, padding=p).permute(0, 2, 3, 1)
+    assert got.shape == ref.shape
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_conv_vae_downsample_asym_pad(device, dt):
+    # F.pad(x, (0,1,0,1)) + 3x3 stride 2 pad 0 (AutoencoderKL Downsample2D, padding=0)
+    x = _r(2, 64, 18, 14, seed=4)
+    w = _r(64, 64, 3, 3, seed=5, scale=0.05)
+    b = _r(64, seed=6)
+    Ho, Wo = (18 + 1 - 3) // 2 + 1, (14 + 1 - 3) // 2 + 1
+    got = O.conv2d(_dev(x.permute(0, 2, 3, 1), dt, device), w.to(dt).float(), b, stride=2, pad=(0, 0),
+                   out_hw=(Ho, Wo))
+    ref = F.conv2d(F.pad(_q(x, dt), (0, 1, 0, 1)), _q(w, dt), b, stride=2).permute(0, 2, 3, 1)
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("src_hw,dst_hw", [((8, 8), (16, 16)), ((6, 4), (11, 7)), ((5, 6), (10, 12))])
+def test_conv_fused_upsample(device, dt, src_hw, dst_hw):
+    # Upsample2D: nearest resize (x2 or to the skip size) fused into the following 3x3 conv
+    x = _r(2, 32, *src_hw, seed=7)
+    w = _r(48, 32, 3, 3, seed=8, scale=0.06)
+    b = _r(48, seed=9)
+    got = O.conv2d(_dev(x.permute(0, 2, 3, 1), dt, device), w.to(dt).float(), b, up_hw=dst_hw)
+    up = F.interpolate(_q(x, dt), size=dst_hw, mode="nearest")
+    ref = F.conv2d(up, _q(w, dt), b, padding=1).permute(0, 2, 3, 1)
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("k", [1, 3])
+def test_conv_concat_rowadd_residual(device, dt, k):
+    # up-block resnet: cat([h, skip]) read from two sources; + time-embedding row add; + residual
+    N, H, W, C0, C1, Co = 2, 10, 9, 64, 32, 80
+    x0, x1 = _r(N, C0, H, W, seed=10), _r(N, C1, H, W, seed=11)
+    w = _r(Co, C0 + C1, k, k, seed=12, scale=0.05)
+    b = _r(Co, seed=13)
+    temb = _r(N, Co + 16, seed=14)             # padded row stride like the fused time_emb_proj output
+    res = _r(N, H, W, Co, seed=15)
+    p = k // 2
+    got = O.conv2d(_dev(x0.permute(0, 2, 3, 1), dt, device), w.to(dt).float(), b, pad=(p, p),
+                   x1=_dev(x1.permute(0, 2, 3, 1), dt, device), rowadd=temb.to(device).contiguous(),
+                   residual=_dev(res, dt, device))
+    ref = F.conv2d(torch.cat([_q(x0, dt), _q(x1, dt)], 1), _q(w, dt), b, padding=p)
+    ref = ref + temb[:, :Co, None, None]
+    ref = ref.permute(0, 2, 3, 1) + _q(res, dt)
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("M,N,K", [(4096, 320, 320), (77, 2304, 768), (300, 2560, 320), (16, 1280, 320),
+                                   (1024, 640, 2560), (5, 24, 8)])
+def test_gemm(device, dt, M, N, K):
+    A = _r(M, K, seed=20)
+    Bw = _r(N, K, seed=21, scale=1 / math.sqrt(K))
+    bias = _r(N, seed=22)
+    got = O.gemm(_dev(A, dt, device), _dev(Bw, dt, device), bias=bias.to(device))
+    ref = _q(A, dt) @ _q(Bw, dt).T + bias
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("act", [1, 2, 3])
+def test_gemm_act_residual_f32out(device, dt, act):
+    M, N, K = 200, 96, 64
+    A, Bw, bias, res = _r(M, K, seed=23), _r(N, K, seed=24, scale=0.2), _r(N, seed=25), _r(M, N, seed=26)
+    got = O.gemm(_dev(A, dt, device), _dev(Bw, dt, device), bias=bias.to(device), act=act,
+                 residual=_dev(res, dt, device), out_f32=True, alpha=0.5)
+    y = 0.5 * (_q(A, dt) @ _q(Bw, dt).T) + bias
+    y = {1: F.silu, 2: F.gelu, 3: lambda v: v * torch.sigmoid(1.702 * v)}[act](y)
+    ref = y + _q(res, dt)
+    assert got.dtype == torch.float32
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_gemm_batched(device, dt):
+    b, M, N, K = 3, 130, 70, 64
+    A, Bw = _r(b, M, K, seed=27), _r(b, N, K, seed=28, scale=0.2)
+    got = O.gemm(_dev(A, dt, device), _dev(Bw, dt, device), batch=b, out_f32=True)
+    ref = torch.bmm(_q(A, dt), _q(Bw, dt).transpose(1, 2))
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("C0,C1,H,W,silu,eps", [(320, 0, 16, 16, True, 1e-5), (1280, 640, 8, 8, True, 1e-5),
+                                                (128, 0, 33, 20, False, 1e-6), (640, 0, 7, 5, False, 1e-6),
+                                                (2560, 0, 4, 4, True, 1e-5)])
+def test_group_norm(device, dt, C0, C1, H, W, silu, eps):
+    N = 2
+    x0 = _r(N, C0, H, W, seed=30) * 3 + 1.5        # offset mean: exercises the variance path
+    x1 = _r(N, C1, H, W, seed=31) if C1 else None
+    g, b = 1 + 0.1 * _r(C0 + C1, seed=32), 0.1 * _r(C0 + C1, seed=33)
+    got = O.group_norm(_dev(x0.permute(0, 2, 3, 1), dt, device), g.to(device), b.to(device), eps, silu=silu,
+                       x1=_dev(x1.permute(0, 2, 3, 1), dt, device) if C1 else None)
+    xin = torch.cat([_q(x0, dt)] + ([_q(x1, dt)] if C1 else []), 1)
+    ref = F.group_norm(xin, 32, g, b, eps)
+    ref = (F.silu(ref) if silu else ref).permute(0, 2, 3, 1)
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("rows,Cc", [(4096, 320), (154, 768), (64, 1280), (3, 640)])
+def test_layer_norm(device, dt, rows, Cc):
+    x = _r(rows, Cc, seed=40) * 2 + 0.5
+    g, b = 1 + 0.1 * _r(Cc, seed=41), 0.1 * _r(Cc, seed=42)
+    got = O.layer_norm(_dev(x, dt, device), g.to(device), b.to(device), 1e-5)
+    ref = F.layer_norm(_q(x, dt), (Cc,), g, b, 1e-5)
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("B,Lq,Lk,C,heads,causal", [
+    (2, 256, 256, 320, 8, False),     # d = 40 self-attention
+    (2, 200, 77, 320, 8, False),      # cross-attention, ragged Lq, Lk = 77
+    (1, 100, 100, 640, 8, False),     # d = 80
+    (2, 64, 77, 1280, 8, False),      # d = 160 cross
+    (1, 300, 300, 1280, 8, False),    # d = 160 self
+    (2, 77, 77, 768, 12, True),       # CLIP causal, d = 64
+])
+def test_attention(device, dt, B, Lq, Lk, C, heads, causal):
+    q, k, v = _r(B, Lq, C, seed=50), _r(B, Lk, C, seed=51), _r(B, Lk, C, seed=52)
+    got = O.attention(_dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device), heads, causal)
+    ref = O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), heads, causal)
+    assert O.rel_err(got, ref) < TOL[dt] * (2 if dt == torch.bfloat16 else 1)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_attention_fused_qkv_strides(device, dt):
+    # q|k|v packed in one [B, L, 3C] buffer (the engine's fused projection)
+    B, Lq, C, heads = 2, 130, 640, 8
+    qkv = _dev(_r(B, Lq, 3 * C, seed=53), dt, device)
+    got = O.attention(qkv[:, :, :C], qkv[:, :, C:2 * C], qkv[:, :, 2 * C:], heads)
+    c = qkv.float().cpu()
+    ref = O.ref_attention(c[:, :, :C], c[:, :, C:2 * C], c[:, :, 2 * C:], heads)
+    assert O.rel_err(got, ref) < TOL[dt] * (2 if dt == torch.bfloat16 else 1)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_attention_softmax_spike(device, dt):
+    # a key whose score dwarfs the rest, arriving in a late tile: forces the online-softmax rescale
+    B, L, C, heads = 1, 256, 320, 8
+    q, k, v = _r(B, L, C, seed=54), _r(B, L, C, seed=55), _r(B, L, C, seed=56)
+    k[:, 200] = q[:, 3] * 4.0
+    got = O.attention(_dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device), heads)
+    ref = O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), heads)
+    assert O.rel_err(got, ref) < TOL[dt] * (2 if dt == torch.bfloat16 else 1)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_geglu(device, dt):
+    x = _r(300, 2 * 1280, seed=60)
+    got = O.geglu(_dev(x, dt, device))
+    h, g = _q(x, dt).chunk(2, dim=-1)
+    ref = h * F.gelu(g)
+    assert O.rel_err(got, ref) < TOL[dt]
