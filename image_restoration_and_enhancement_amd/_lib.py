@@ -57,6 +57,10 @@ vp, i32, f32, sz, i64 = C.c_void_p, C.c_int, C.c_float, C.c_size_t, C.c_long
 _SIGS = {
     "irx_last_error": (C.c_char_p, []),
     "irx_version": (i32, []),
+    "irx_profile_begin": (i32, []),
+    "irx_profile_end": (i32, [C.POINTER(i32)]),
+    "irx_profile_get": (i32, [i32, C.POINTER(C.c_char_p), C.POINTER(C.c_long), C.POINTER(C.c_double),
+                              C.POINTER(C.c_double)]),
     "irx_model_create": (i32, [i32, C.POINTER(ModelConfig), i32, C.POINTER(vp)]),
     "irx_model_destroy": (i32, [vp]),
     "irx_model_num_params": (i32, [vp, C.POINTER(i32)]),
@@ -120,6 +124,22 @@ def call(name: str, *args):
     if _SIGS[name][0] is i32 and name not in ("irx_version",) and rc != 0:
         raise IrxError(f"{name}: {lib.irx_last_error().decode(errors='replace')}")
     return rc
+
+
+def profile_begin() -> None:
+    call("irx_profile_begin")
+
+
+def profile_end() -> list:
+    """[(kernel name, launches, total ms, total algorithmic flops)] since profile_begin()."""
+    n = C.c_int()
+    call("irx_profile_end", C.byref(n))
+    out = []
+    for i in range(n.value):
+        name, cnt, ms, fl = C.c_char_p(), C.c_long(), C.c_double(), C.c_double()
+        call("irx_profile_get", i, C.byref(name), C.byref(cnt), C.byref(ms), C.byref(fl))
+        out.append((name.value.decode(), int(cnt.value), float(ms.value), float(fl.value)))
+    return out
 
 
 def ptr(t) -> int | None:

@@ -10,6 +10,7 @@
 // bf16: v_mfma_f32_16x16x16_bf16 (K = 16 keeps d = 40 / 80 padding at 48 / 80);
 // fp32 (parity mode): exact-f32 v_mfma_f32_16x16x4_f32.
 #include "ops.h"
+#include "profile.h"
 
 namespace irx {
 namespace {
@@ -247,6 +248,10 @@ template <typename T>
 void launch_t(const AttnArgs& a, hipStream_t s) {
   dim3 grid((a.Lq + kQB - 1) / kQB, a.H, a.B), block(256);
   const int dp = (a.d + 15) / 16 * 16;
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn_kernel<") +
+                               (sizeof(T) == 2 ? "unsigned short" : "float") + ", " + std::to_string(dp) + ">"
+                         : std::string(),
+               4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
   switch (dp) {
     case 48: attn_kernel<T, 48><<<grid, block, 0, s>>>(a); break;
     case 64: attn_kernel<T, 64><<<grid, block, 0, s>>>(a); break;

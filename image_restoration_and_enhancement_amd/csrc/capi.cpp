@@ -6,6 +6,7 @@
 
 #include "../../include/irx.h"
 #include "models.h"
+#include "profile.h"
 
 namespace irx {
 static thread_local std::string g_err;
@@ -51,6 +52,24 @@ extern "C" {
 
 const char* irx_last_error(void) { return last_error(); }
 int irx_version(void) { return 1; }
+
+int irx_profile_begin(void) {
+  IRX_API_BEGIN
+  prof_begin();
+  IRX_API_END
+}
+int irx_profile_end(int* n) {
+  IRX_API_BEGIN
+  IRX_CHECK(n, "null argument");
+  *n = prof_end();
+  IRX_API_END
+}
+int irx_profile_get(int i, const char** name, long* launches, double* ms, double* flops) {
+  IRX_API_BEGIN
+  IRX_CHECK(name && launches && ms && flops, "null argument");
+  IRX_CHECK(prof_get(i, name, launches, ms, flops), "profile index out of range");
+  IRX_API_END
+}
 
 int irx_model_create(int kind, const irx_model_config* cfg, int dtype, irx_model** out) {
   IRX_API_BEGIN

@@ -12,6 +12,7 @@
 // per K step, next tile's loads in flight under the current tile's MFMAs) with a bank-spreading
 // XOR swizzle; block -> tile mapping is XCD-aware.
 #include "ops.h"
+#include "profile.h"
 
 namespace irx {
 
@@ -221,11 +222,21 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs a) {
   }
 }
 
+// kernel instantiation name as rocprofv3 prints it (demangled), used by the in-process profiler
+template <typename T, int WM, int WN, int TM, int TN>
+std::string kname(bool conv, bool f32out) {
+  return std::string("irx::(anonymous namespace)::gemm_kernel<") + (sizeof(T) == 2 ? "unsigned short" : "float") +
+         ", " + std::to_string(WM) + ", " + std::to_string(WN) + ", " + std::to_string(TM) + ", " +
+         std::to_string(TN) + ", " + (conv ? "true" : "false") + ", " + (f32out ? "true" : "false") + ">";
+}
+
 template <typename T, int WM, int WN, int TM, int TN>
 void launch_cfg(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, a.batch), block(kThreads);
+  ProfScope ps(prof_on() ? kname<T, WM, WN, TM, TN>(a.conv, a.out_f32) : std::string(),
+               2.0 * a.M * a.N * (double)a.K * a.batch, s);
   if (a.conv) {
     if (a.out_f32) gemm_kernel<T, WM, WN, TM, TN, true, true><<<grid, block, 0, s>>>(a);
     else gemm_kernel<T, WM, WN, TM, TN, true, false><<<grid, block, 0, s>>>(a);

@@ -69,6 +69,11 @@ typedef struct {
 const char* irx_last_error(void);
 int irx_version(void);
 
+/* ---- optional per-launch HIP-event timing of the MFMA kernels (bench.py roofline) ---- */
+int irx_profile_begin(void);
+int irx_profile_end(int* n_kernels);   /* synchronises, aggregates per kernel instantiation */
+int irx_profile_get(int i, const char** name, long* launches, double* total_ms, double* total_flops);
+
 /* ---- model lifetime: replaces diffusers/transformers from_pretrained (src/inference.py:162-172) ---- */
 int irx_model_create(int kind, const irx_model_config* cfg, int dtype, irx_model** out);
 int irx_model_destroy(irx_model* m);
