@@ -15,6 +15,7 @@ LIB_PATH = Path(os.environ.get("IRX_LIB", _PKG / "libirx.so"))
 IRX_F32, IRX_BF16 = 0, 1
 IRX_MODEL_UNET, IRX_MODEL_VAE, IRX_MODEL_CLIP = 0, 1, 2
 IRX_LAYOUT_VEC, IRX_LAYOUT_MAT, IRX_LAYOUT_CONV, IRX_LAYOUT_EMB = 0, 1, 2, 3
+IRX_LAYOUT_MAT_GEGLU64, IRX_LAYOUT_VEC_GEGLU64 = 4, 5
 
 
 class IrxError(RuntimeError):
@@ -57,6 +58,7 @@ vp, i32, f32, sz, i64 = C.c_void_p, C.c_int, C.c_float, C.c_size_t, C.c_long
 _SIGS = {
     "irx_last_error": (C.c_char_p, []),
     "irx_version": (i32, []),
+    "irx_set_option": (i32, [C.c_char_p, i32]),
     "irx_profile_begin": (i32, []),
     "irx_profile_end": (i32, [C.POINTER(i32)]),
     "irx_profile_get": (i32, [i32, C.POINTER(C.c_char_p), C.POINTER(C.c_long), C.POINTER(C.c_double),
@@ -94,6 +96,7 @@ _SIGS = {
     "irx_op_attention": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp,
                                i64, i64, f32, i32]),
     "irx_op_geglu": (i32, [vp, i32, vp, i32, i32, vp]),
+    "irx_op_gemm_geglu": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, vp]),
 }
 
 EXPORTED = tuple(_SIGS)

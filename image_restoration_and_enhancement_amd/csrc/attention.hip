@@ -85,38 +85,67 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
 #pragma unroll
   for (int j = 0; j < kQT; ++j) { mrow[j] = -INFINITY; lrow[j] = 0.f; }
 
-  const float sl2 = a.scale * 1.4426950408889634f;
+  const float sl2 = a.scale * 1.4426950408889634f;   // softmax in base 2: exp(x*scale) = exp2(x*sl2)
   int kend = a.Lk;
   if (a.causal) kend = min(kend, qb0 + kQB);
   const int cpr = d * (int)sizeof(T) / 16;           // 16-byte chunks per K/V row
+  constexpr int E = 16 / (int)sizeof(T);
+  // bf16: the next K/V tile is fetched into registers under the current tile's MFMAs (async-STAGE split);
+  // fp32 (parity mode, register-bound at d = 160): synchronous staging.
+  constexpr bool PREFETCH = sizeof(T) == 2;
+  constexpr int NCH = PREFETCH ? (kKT * (DP * (int)sizeof(T) / 16) + 255) / 256 : 1;
+  uint4 kreg[NCH], vreg[NCH];
+  auto load_regs = [&](int j0) {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = tid + 256 * u;
+      kreg[u] = make_uint4(0, 0, 0, 0);
+      vreg[u] = make_uint4(0, 0, 0, 0);
+      if (idx < kKT * cpr) {
+        const int r = idx / cpr, c = idx - r * cpr;
+        const int key = j0 + r;
+        if (key < a.Lk) {
+          kreg[u] = *(const uint4*)(K + (long)key * a.ldk + c * E);
+          vreg[u] = *(const uint4*)(V + (long)key * a.ldv + c * E);
+        }
+      }
+    }
+  };
+  auto store_regs = [&]() {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = tid + 256 * u;
+      if (idx < kKT * cpr) {
+        const int r = idx / cpr, c = idx - r * cpr;
+        *(uint4*)(Ks + r * SK + c * E) = kreg[u];
+        *(uint4*)(Vs + r * SV + c * E) = vreg[u];
+      }
+    }
+  };
+  if constexpr (PREFETCH) load_regs(0);
 
   for (int j0 = 0; j0 < kend; j0 += kKT) {
     __syncthreads();   // previous tile fully consumed
-    for (int idx = tid; idx < kKT * cpr; idx += 256) {
-      const int r = idx / cpr, c = idx - r * cpr;
-      const int key = j0 + r;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-      if (key < a.Lk) {
-        kv = *(const uint4*)(K + (long)key * a.ldk + c * (16 / (int)sizeof(T)));
-        vv = *(const uint4*)(V + (long)key * a.ldv + c * (16 / (int)sizeof(T)));
-      }
-      constexpr int E = 16 / (int)sizeof(T);
-      if constexpr (sizeof(T) == 2) {
-        *(uint4*)(Ks + r * SK + c * E) = kv;       // SK*2 bytes is a multiple of 16
-        if constexpr ((SV * 2) % 16 == 0) {
-          *(uint4*)(Vs + r * SV + c * E) = vv;
-        } else {
-          uint2* p = (uint2*)(Vs + r * SV + c * E);
-          p[0] = make_uint2(vv.x, vv.y); p[1] = make_uint2(vv.z, vv.w);
+    if constexpr (PREFETCH) {
+      store_regs();
+      __syncthreads();
+      if (j0 + kKT < kend) load_regs(j0 + kKT);
+    } else {
+      for (int idx = tid; idx < kKT * cpr; idx += 256) {
+        const int r = idx / cpr, c = idx - r * cpr;
+        const int key = j0 + r;
+        uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+        if (key < a.Lk) {
+          kv = *(const uint4*)(K + (long)key * a.ldk + c * E);
+          vv = *(const uint4*)(V + (long)key * a.ldv + c * E);
         }
-      } else {
         *(uint4*)(Ks + r * SK + c * E) = kv;
         float* pv = (float*)(Vs + r * SV + c * E);
         pv[0] = __uint_as_float(vv.x); pv[1] = __uint_as_float(vv.y);
         pv[2] = __uint_as_float(vv.z); pv[3] = __uint_as_float(vv.w);
       }
+      __syncthreads();
     }
-    __syncthreads();
 
     // ---- S^T = K Q^T  (rows = keys of this tile, cols = this wave's queries)
     f32x4 s[4][kQT];
@@ -149,24 +178,31 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
     // ---- online softmax per query column
     typedef typename std::conditional<sizeof(T) == 2, s16x4, f32x4>::type pfrag_t;
     pfrag_t pf[4][kQT];
+    // masking only on tiles that reach past Lk or (causal) past the wave's first query
+    const bool need_mask = (j0 + kKT > a.Lk) || (a.causal && j0 + kKT - 1 > q0);
 #pragma unroll
     for (int qt = 0; qt < kQT; ++qt) {
       const int q = q0 + qt * 16 + li;
-      float tmax = -INFINITY;
+      if (need_mask) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = j0 + kt * 16 + 4 * g + i;
+            if (key >= a.Lk || (a.causal && key > q)) s[kt][qt][i] = -INFINITY;
+          }
+      }
+      float tmax = -INFINITY;     // max of the raw scores (scale > 0 commutes with max)
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = j0 + kt * 16 + 4 * g + i;
-          float x = s[kt][qt][i] * sl2;
-          if (key >= a.Lk || (a.causal && key > q)) x = -INFINITY;
-          s[kt][qt][i] = x;
-          tmax = fmaxf(tmax, x);
-        }
+        for (int i = 0; i < 4; ++i) tmax = fmaxf(tmax, s[kt][qt][i]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
       const float mnew = fmaxf(mrow[qt], tmax);
-      const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(mrow[qt] - mnew);
+      const bool none = mnew == -INFINITY;           // every key so far masked
+      const float alpha = none ? 1.f : exp2f((mrow[qt] - mnew) * sl2);
+      const float nb = none ? 0.f : -mnew * sl2;
       mrow[qt] = mnew;
       float lsum = 0.f;
 #pragma unroll
@@ -174,7 +210,7 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
         float p[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          p[i] = (mnew == -INFINITY) ? 0.f : exp2f(s[kt][qt][i] - mnew);
+          p[i] = exp2f(fmaf(s[kt][qt][i], sl2, nb));
           lsum += p[i];
         }
         if constexpr (sizeof(T) == 2) {

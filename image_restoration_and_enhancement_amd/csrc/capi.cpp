@@ -53,6 +53,15 @@ extern "C" {
 const char* irx_last_error(void) { return last_error(); }
 int irx_version(void) { return 1; }
 
+int irx_set_option(const char* name, int value) {
+  IRX_API_BEGIN
+  IRX_CHECK(name, "null option name");
+  const std::string n(name);
+  if (n == "large_tiles") g_large_tiles = value != 0;
+  else throw Error("unknown option " + n);
+  IRX_API_END
+}
+
 int irx_profile_begin(void) {
   IRX_API_BEGIN
   prof_begin();
@@ -329,10 +338,22 @@ int irx_op_attention(void* s, int dtype, int B, int H, int lq, int lk, int d, co
   IRX_API_END
 }
 
+int irx_op_gemm_geglu(void* s, int dtype, int M, int N, int K, const void* A, const void* B, const float* bias,
+                      void* C) {
+  IRX_API_BEGIN
+  GemmArgs a;
+  a.dtype = dtype; a.M = M; a.N = N; a.K = K;
+  a.A = A; a.lda = K; a.B = B; a.ldb = K;
+  a.C = C; a.ldc = N / 2; a.bias = bias; a.geglu = 1;
+  IRX_CHECK(gemm_geglu_fusable(a), "shape/dtype not eligible for the fused GEGLU epilogue");
+  gemm(a, S(s));
+  IRX_API_END
+}
+
 int irx_op_geglu(void* s, int dtype, const void* proj, int M, int F, void* out) {
   IRX_API_BEGIN
   IRX_CHECK(proj && out, "null buffer");
-  geglu(dtype, proj, 2L * F, M, F, out, F, S(s));
+  geglu(dtype, proj, 2L * F, M, F, out, F, 0, S(s));
   IRX_API_END
 }
 

@@ -12,15 +12,19 @@ inline int nblk(long n, int per = kB) { return (int)((n + per - 1) / per); }
 
 // ------------------------------------------------------------------ GEGLU: h * gelu_erf(gate)
 template <typename T>
-__global__ void geglu_kernel(const T* __restrict__ p, long ldp, int M, int F, T* __restrict__ o, long ldo) {
+__global__ void geglu_kernel(const T* __restrict__ p, long ldp, int M, int F, T* __restrict__ o, long ldo,
+                             int il) {
   constexpr int VEC = 16 / (int)sizeof(T);
   const int nv = F / VEC;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)M * nv) return;
   const int m = (int)(i / nv), v = (int)(i % nv);
+  const int f = v * VEC;
+  const int hc = il ? (f / 64) * 128 + (f % 64) : f;
+  const int gc = il ? hc + 64 : F + f;
   float h[VEC], g[VEC];
-  Vec16<T>::unpack(*(const uint4*)(p + (long)m * ldp + v * VEC), h);
-  Vec16<T>::unpack(*(const uint4*)(p + (long)m * ldp + F + v * VEC), g);
+  Vec16<T>::unpack(*(const uint4*)(p + (long)m * ldp + hc), h);
+  Vec16<T>::unpack(*(const uint4*)(p + (long)m * ldp + gc), g);
 #pragma unroll
   for (int e = 0; e < VEC; ++e) h[e] = h[e] * gelu_erf(g[e]);
   *(uint4*)(o + (long)m * ldo + v * VEC) = Vec16<T>::pack(h);
@@ -261,11 +265,12 @@ __global__ void scale_copy_kernel(const float* __restrict__ in, long npix, float
 
 }  // namespace
 
-void geglu(int dtype, const void* proj, long ldp, int M, int F, void* out, long ldo, hipStream_t s) {
+void geglu(int dtype, const void* proj, long ldp, int M, int F, void* out, long ldo, int il, hipStream_t s) {
   const int vec = dtype == F32 ? 4 : 8;
   IRX_CHECK(F % vec == 0 && ldp % vec == 0 && ldo % vec == 0, "geglu alignment");
+  IRX_CHECK(!il || F % 64 == 0, "interleaved geglu needs F % 64 == 0");
   const long n = (long)M * (F / vec);
-  IRX_DISPATCH(dtype, (geglu_kernel<T><<<nblk(n), kB, 0, s>>>((const T*)proj, ldp, M, F, (T*)out, ldo)));
+  IRX_DISPATCH(dtype, (geglu_kernel<T><<<nblk(n), kB, 0, s>>>((const T*)proj, ldp, M, F, (T*)out, ldo, il)));
 }
 
 void timestep_embed(int dtype, const float* t, int B, int dim, int flip, float shift, void* out, hipStream_t s) {

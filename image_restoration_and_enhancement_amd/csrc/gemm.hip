@@ -257,6 +257,8 @@ void launch_t(const GemmArgs& a, hipStream_t s) {
 
 }  // namespace
 
+bool g_large_tiles = true;   // irx_set_option("large_tiles", 0) forces the 4-wave kernel (A/B tests)
+
 void gemm(const GemmArgs& a, hipStream_t s) {
   const int vec = a.dtype == F32 ? 4 : 8;
   IRX_CHECK(a.M > 0 && a.N > 0 && a.K > 0, "empty GEMM");
@@ -274,8 +276,12 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   } else {
     IRX_CHECK(a.A && a.lda % vec == 0 && ((uintptr_t)a.A % 16) == 0, "A rows must be 16-byte aligned");
   }
+  if (a.geglu) {
+    IRX_CHECK(gemm_geglu_fusable(a) && gemm_large_tile(a, s), "GEGLU epilogue needs the large-tile path");
+    return;
+  }
   if (a.dtype == F32) launch_t<float>(a, s);
-  else launch_t<bf16_t>(a, s);
+  else if (!(g_large_tiles && gemm_large_tile(a, s))) launch_t<bf16_t>(a, s);
 }
 
 }  // namespace irx

@@ -1,0 +1,476 @@
+// irx — large-tile bf16 MFMA GEMM / implicit-GEMM convolution (8 waves, LDS-DMA staging), gfx950.
+//
+// The throughput path for the big contractions of the UNet and VAE (M = pixels in the thousands to
+// hundreds of thousands, N = Cout in {128 .. 10240}, K = 9*Cin or Cin):
+//   * 512-thread workgroups (8 waves, 2 per SIMD), block tiles 256x256 / 128x320 / 256x128 / 128x256 /
+//     128x128 chosen per call so N = 320/640/960/1280/2560 and 128/256/512 tile exactly and the grid
+//     fills the 256 CUs (split-K with an fp32 partial-sum pass when the output has too few tiles);
+//   * A and B staged global -> LDS with 16-byte global_load_lds (LDS-DMA, no VGPR round trip):
+//     the im2col gather of a 3x3 / strided / upsampled / concatenated convolution is just a per-lane
+//     source address (out-of-image taps and rows past M/N point at a zero page);
+//   * LDS image written lane-linearly, bank-spread by an XOR swizzle applied on the SOURCE address
+//     and undone on the ds_read_b128 fragment reads; two LDS stages: the DMA of K step k+1 is in
+//     flight under the 2 x (TM x TN) v_mfma_f32_16x16x32_bf16 of step k, one barrier per step;
+//   * epilogue staged through LDS one slab at a time and written as whole 16-byte row chunks
+//     (bias / time-embedding row add / activation / residual fused);
+//   * XCD-aware block -> tile mapping (tiles sharing an A panel on one XCD's L2).
+// Requirements (else the 4-wave kernel in gemm.hip runs): bf16, K % 64 == 0, conv channel
+// counts % 64 == 0 (a 64-deep K step never straddles a tap or the concat seam).
+#include <mutex>
+
+#include "ops.h"
+#include "profile.h"
+
+namespace irx {
+
+__device__ uint4 g_zero_page[4];   // 64 zero bytes: the source of every padded / out-of-range lane
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+struct Split {
+  int splits = 1;      // K splits (gridDim.y = batch * splits)
+  int per = 0;         // K steps per split
+  float* ws = nullptr; // fp32 partials [batch*splits][M][N]
+};
+
+template <int BM, int BN, int WM, int WN, bool CONV, bool OUTF32, bool RESIZE>
+__global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int ROWS = BM + BN;
+  constexpr int NINST = ROWS / 8;            // 1 KiB LDS-DMA wave instructions per stage (8 rows each)
+  constexpr int IPW = NINST / 8;             // per wave
+  static_assert(WM * WN == 8 && NINST % 8 == 0 && BM % 64 == 0, "tile shape");
+  __shared__ __attribute__((aligned(16))) uint4 smem[2 * ROWS * 8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = a.N / BN + (a.N % BN != 0);
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tile_n = bid % tiles_n, tile_m = bid / tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int z = blockIdx.y / sp.splits, ks = blockIdx.y % sp.splits;
+  const int nk_all = a.K / 64;
+  const int kt0 = ks * sp.per;
+  const int kt1 = min(nk_all, kt0 + sp.per);
+  const uint16_t* __restrict__ Bp = (const uint16_t*)a.B + (long)z * a.sB;
+  const uint16_t* __restrict__ Ap = CONV ? nullptr : (const uint16_t*)a.A + (long)z * a.sA;
+  const uint16_t* zp = (const uint16_t*)g_zero_page;
+
+  // ---- per-lane DMA assignment: instruction j of this wave covers rows 8*(wave*IPW + j) .. +7;
+  //      lane -> row + 16-byte slot; it fetches the logical chunk slot ^ swz(row)
+  // Each lane keeps a row base pointer (nullptr = zero page) and adds a block-uniform K offset per step;
+  // conv rows re-derive their base only when the K walk enters a new tap or the concat's second source.
+  const int lrow = lane >> 3, lslot = lane & 7;
+  bool isA[IPW];
+  int lk[IPW];                       // this lane's element offset in the 64-deep K step (logical chunk * 8)
+  int rn[IPW], riy[IPW], rix[IPW];   // conv A rows: image index (-1 invalid), receptive-field origin
+  const uint16_t* rb[IPW];           // current row base (nullptr if out of range / padded tap)
+#pragma unroll
+  for (int j = 0; j < IPW; ++j) {
+    const int r = 8 * (wave * IPW + j) + lrow;
+    isA[j] = r < BM;
+    lk[j] = (lslot ^ ((r >> 1) & 7)) * 8;
+    rn[j] = -1; riy[j] = 0; rix[j] = 0; rb[j] = nullptr;
+    if (r < BM) {
+      const int m = m0 + r;
+      if (m < a.M) {
+        if constexpr (CONV) {
+          const int HWo = a.g.Ho * a.g.Wo;
+          const int n = m / HWo, rem = m - n * HWo;
+          const int oy = rem / a.g.Wo, ox = rem - oy * a.g.Wo;
+          rn[j] = n;
+          riy[j] = oy * a.g.stride - a.g.pad_t;
+          rix[j] = ox * a.g.stride - a.g.pad_l;
+        } else {
+          rb[j] = Ap + (long)m * a.lda;
+        }
+      }
+    } else {
+      const int n = n0 + (r - BM);
+      if (n < a.N) rb[j] = Bp + (long)n * a.ldb;
+    }
+  }
+  const float sy = RESIZE ? (float)a.g.Hin / (float)a.g.Hv : 1.f;
+  const float sx = RESIZE ? (float)a.g.Win / (float)a.g.Wv : 1.f;
+  const int Cin = a.g.C0 + a.g.C1;
+  // conv: channel / tap of the K step being issued (block-uniform)
+  int kc = 0, ky = 0, kx = 0;
+  auto retarget = [&]() {   // A-row bases for tap (ky, kx) and the source holding channel kc
+    const bool second = kc >= a.g.C0;
+    const uint16_t* sb = second ? (const uint16_t*)a.g.src1 : (const uint16_t*)a.g.src0;
+    const int cs = second ? a.g.C1 : a.g.C0;
+#pragma unroll
+    for (int j = 0; j < IPW; ++j) {
+      if (!isA[j]) continue;
+      int iy = riy[j] + ky, ix = rix[j] + kx;
+      const bool ok = rn[j] >= 0 && iy >= 0 && iy < a.g.Hv && ix >= 0 && ix < a.g.Wv;
+      if constexpr (RESIZE) {
+        iy = (a.g.Hv == 2 * a.g.Hin) ? (iy >> 1) : min((int)((float)iy * sy), a.g.Hin - 1);
+        ix = (a.g.Wv == 2 * a.g.Win) ? (ix >> 1) : min((int)((float)ix * sx), a.g.Win - 1);
+      }
+      const long pix = ((long)rn[j] * a.g.Hin + iy) * a.g.Win + ix;
+      rb[j] = ok ? sb + pix * cs : nullptr;
+    }
+  };
+  if constexpr (CONV) {
+    const int k = kt0 * 64;
+    const int tap = k / Cin;
+    kc = k - tap * Cin;
+    ky = tap / a.g.KW;
+    kx = tap - ky * a.g.KW;
+    retarget();
+  }
+
+  auto issue = [&](int kt, int stage) {
+    uint4* sbase = smem + stage * ROWS * 8;
+    const int koffA = CONV ? (kc >= a.g.C0 ? kc - a.g.C0 : kc) : kt * 64;
+    const int koffB = kt * 64;
+#pragma unroll
+    for (int j = 0; j < IPW; ++j) {
+      const uint16_t* src = rb[j] ? rb[j] + ((isA[j] ? koffA : koffB) + lk[j]) : zp;
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(sbase + (wave * IPW + j) * 64), 16, 0, 0);
+    }
+    if constexpr (CONV) {
+      kc += 64;
+      if (kc == Cin) {
+        kc = 0;
+        if (++kx == a.g.KW) { kx = 0; ++ky; }
+        retarget();
+      } else if (kc == a.g.C0) {
+        retarget();
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fgrp = lane >> 4;
+  if (kt0 < kt1) issue(kt0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int st = (kt - kt0) & 1;
+    if (kt + 1 < kt1) issue(kt + 1, st ^ 1);
+    const uint4* As = smem + st * ROWS * 8;
+    const uint4* Bs = As + BM * 8;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      uint4 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * TM * 16 + i * 16 + frow;
+        af[i] = As[r * 8 + ((s * 4 + fgrp) ^ ((r >> 1) & 7))];
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * TN * 16 + j * 16 + frow;
+        bfr[j] = Bs[r * 8 + ((s * 4 + fgrp) ^ (((r + BM) >> 1) & 7))];
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                              __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- split-K: raw fp32 partial tile, epilogue applied by splitk_reduce_kernel
+  if (sp.splits > 1) {
+    float* P = sp.ws + (long)blockIdx.y * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * TN * 16 + j * 16 + frow;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * TM * 16 + i * 16 + fgrp * 4 + r;
+          if (m < a.M && n < a.N) P[(long)m * a.N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+
+  // ---- epilogue (D[row = 4g + r][col = lane & 15] per 16x16 tile)
+  const uint16_t* __restrict__ Rp = a.residual ? (const uint16_t*)a.residual + (long)z * a.sR : nullptr;
+  if constexpr (!OUTF32) {
+    if (a.vec_epilogue) {
+      // Staged through LDS: pass 1 (every wave) applies alpha/bias/row-add/act and writes the bf16 tile
+      // (16-byte chunks XOR-swizzled by row to spread banks); pass 2 streams whole 16-byte row chunks out,
+      // adding the residual and applying out_scale, or (GEGLU) combining each 64-wide value block with its
+      // gate block h * gelu(g) and writing half-width rows.
+      static_assert(BM * BN * 2 <= 2 * ROWS * 8 * 16, "epilogue tile must fit the staging LDS");
+      uint16_t* tileS = (uint16_t*)smem;
+      uint16_t* Cp = (uint16_t*)a.C + (long)z * a.sC;
+      const int act1 = a.geglu ? (int)ACT_NONE : a.act;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * TN * 16 + j * 16 + frow;
+        const float bias = (a.bias && n0 + col < a.N) ? a.bias[n0 + col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = wm * TM * 16 + i * 16 + fgrp * 4 + r;
+            float v = acc[i][j][r] * a.alpha + bias;
+            if (a.rowadd) {
+              const int m = m0 + row;
+              if (m < a.M && n0 + col < a.N) v += a.rowadd[(long)(m / a.rows_per_group) * a.rowadd_ld + n0 + col];
+            }
+            tileS[row * BN + (((col >> 3) ^ (row & 7)) << 3) + (col & 7)] = f2bf(apply_act(v, act1));
+          }
+      }
+      __syncthreads();
+      constexpr int CPR = BN / 8;               // 16-byte chunks per row
+      if (a.geglu) {
+        // tile columns come in (64 value, 64 gate) pairs; output feature block = n0/2 + 64*pair
+        constexpr int OCPR = CPR / 2;
+        for (int idx = tid; idx < BM * OCPR; idx += 512) {
+          const int row = idx / OCPR, oc = idx - row * OCPR;
+          const int m = m0 + row;
+          const int hc = (oc >> 3) * 16 + (oc & 7);       // value chunk; gate chunk is hc + 8
+          if (m >= a.M || n0 + hc * 8 >= a.N) continue;
+          float h[8], gt[8];
+          Vec16<bf16_t>::unpack(*(const uint4*)(tileS + row * BN + ((hc ^ (row & 7)) << 3)), h);
+          Vec16<bf16_t>::unpack(*(const uint4*)(tileS + row * BN + (((hc + 8) ^ (row & 7)) << 3)), gt);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) h[e] = h[e] * gelu_erf(gt[e]);
+          *(uint4*)(Cp + (long)m * a.ldc + n0 / 2 + oc * 8) = Vec16<bf16_t>::pack(h);
+        }
+        return;
+      }
+      for (int idx = tid; idx < BM * CPR; idx += 512) {
+        const int row = idx / CPR, c = idx - row * CPR;
+        const int m = m0 + row, n = n0 + c * 8;
+        if (m >= a.M || n >= a.N) continue;
+        uint4 u = *(const uint4*)(tileS + row * BN + ((c ^ (row & 7)) << 3));
+        if (Rp || a.out_scale != 1.f) {
+          float f[8];
+          Vec16<bf16_t>::unpack(u, f);
+          if (Rp) {
+            float rv[8];
+            Vec16<bf16_t>::unpack(*(const uint4*)(Rp + (long)m * a.ldr + n), rv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] += rv[e];
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] *= a.out_scale;
+          u = Vec16<bf16_t>::pack(f);
+        }
+        *(uint4*)(Cp + (long)m * a.ldc + n) = u;
+      }
+      return;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * TN * 16 + j * 16 + frow;
+      if (n >= a.N) continue;
+      const float bias = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * TM * 16 + i * 16 + fgrp * 4 + r;
+        if (m >= a.M) continue;
+        float v = acc[i][j][r] * a.alpha + bias;
+        if (a.rowadd) v += a.rowadd[(long)(m / a.rows_per_group) * a.rowadd_ld + n];
+        v = apply_act(v, a.act);
+        if (Rp) v += bf2f(Rp[(long)m * a.ldr + n]);
+        v *= a.out_scale;
+        if constexpr (OUTF32) ((float*)a.C)[(long)z * a.sC + (long)m * a.ldc + n] = v;
+        else ((uint16_t*)a.C)[(long)z * a.sC + (long)m * a.ldc + n] = f2bf(v);
+      }
+    }
+  }
+}
+
+// sum of split-K partials + the full epilogue, 8 outputs (one 16-byte bf16 chunk) per thread
+template <bool OUTF32>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const float* __restrict__ ws, int splits) {
+  const int nv = a.N / 8;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)a.M * nv) return;
+  const int z = blockIdx.y;
+  const int m = (int)(i / nv), n = (int)(i % nv) * 8;
+  float f[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = 0.f;
+  for (int s = 0; s < splits; ++s) {
+    const float4* p = (const float4*)(ws + ((long)(z * splits + s) * a.M + m) * a.N + n);
+    const float4 x = p[0], y = p[1];
+    f[0] += x.x; f[1] += x.y; f[2] += x.z; f[3] += x.w; f[4] += y.x; f[5] += y.y; f[6] += y.z; f[7] += y.w;
+  }
+  float rv[8];
+  if (a.residual) {
+    const uint16_t* R = (const uint16_t*)a.residual + (long)z * a.sR + (long)m * a.ldr + n;
+    Vec16<bf16_t>::unpack(*(const uint4*)R, rv);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float v = f[e] * a.alpha + (a.bias ? a.bias[n + e] : 0.f);
+    if (a.rowadd) v += a.rowadd[(long)(m / a.rows_per_group) * a.rowadd_ld + n + e];
+    v = apply_act(v, a.act);
+    if (a.residual) v += rv[e];
+    f[e] = v * a.out_scale;
+  }
+  if constexpr (OUTF32) {
+    float* C = (float*)a.C + (long)z * a.sC + (long)m * a.ldc + n;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) C[e] = f[e];
+  } else {
+    *(uint4*)((uint16_t*)a.C + (long)z * a.sC + (long)m * a.ldc + n) = Vec16<bf16_t>::pack(f);
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles, a.batch * sp.splits), block(512);
+  std::string nm;
+  if (prof_on())
+    nm = "irx::(anonymous namespace)::gemm2_kernel<" + std::to_string(BM) + ", " + std::to_string(BN) + ", " +
+         std::to_string(WM) + ", " + std::to_string(WN) + ", " + (a.conv ? "true" : "false") + ", " +
+         (a.out_f32 ? "true" : "false") + ">";
+  {
+    ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
+    const bool rs = a.conv && (a.g.Hv != a.g.Hin || a.g.Wv != a.g.Win);
+    if (a.conv) {   // (fp32-output convs never take this path: see eligible())
+      if (rs) gemm2_kernel<BM, BN, WM, WN, true, false, true><<<grid, block, 0, s>>>(a, sp);
+      else gemm2_kernel<BM, BN, WM, WN, true, false, false><<<grid, block, 0, s>>>(a, sp);
+    } else {
+      if (a.out_f32) gemm2_kernel<BM, BN, WM, WN, false, true, false><<<grid, block, 0, s>>>(a, sp);
+      else gemm2_kernel<BM, BN, WM, WN, false, false, false><<<grid, block, 0, s>>>(a, sp);
+    }
+    IRX_LAUNCH_CHECK();
+  }
+  if (sp.splits > 1) {
+    const long n = (long)a.M * (a.N / 8);
+    dim3 g2((unsigned)((n + 255) / 256), a.batch);
+    if (a.out_f32) splitk_reduce_kernel<true><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits);
+    else splitk_reduce_kernel<false><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits);
+    IRX_LAUNCH_CHECK();
+  }
+}
+
+// ------------------------------------------------------------------ tile / split policy
+constexpr int kCUs = 256;
+
+struct Choice {
+  int BM = 0, BN = 0, splits = 1, per = 0;
+};
+
+Choice choose(const GemmArgs& a) {
+  Choice best;
+  const int nk = a.K / 64;
+  double best_score = -1.0;
+  const int cands[5][2] = {{256, 256}, {128, 320}, {256, 128}, {128, 256}, {128, 128}};
+  for (auto& c : cands) {
+    const int BM = c[0], BN = c[1];
+    if (a.N % BN != 0) continue;
+    if (a.geglu && BN % 128 != 0) continue;      // tiles must hold whole (value, gate) block pairs
+    const long tiles = (long)((a.M + BM - 1) / BM) * (a.N / BN) * a.batch;
+    const double intensity = (double)BM * BN / (BM + BN) / 128.0;   // 256x256 == 1
+    for (int splits = 1; splits <= 8; splits *= 2) {
+      if (splits > 1 && ((a.out_f32 && a.batch > 1) || a.geglu)) break;
+      const int per = (nk + splits - 1) / splits;
+      if (per < 8 && splits > 1) break;                 // keep >= 8 K steps per split
+      if ((long)(splits - 1) * per >= nk) break;        // no empty split
+      const long blocks = tiles * splits;
+      const double util = (double)blocks / ((double)((blocks + kCUs - 1) / kCUs) * kCUs);
+      // split-K pays an fp32 partial write + read of the output per split
+      const double cost_split = splits > 1 ? 1.0 + 0.06 * splits : 1.0;
+      const double score = util * intensity / cost_split;
+      if (score > best_score + 1e-9) {
+        best_score = score;
+        best.BM = BM; best.BN = BN; best.splits = splits; best.per = per;
+      }
+    }
+  }
+  return best;
+}
+
+std::mutex g_ws_mu;
+float* g_ws = nullptr;
+size_t g_ws_bytes = 0;
+
+float* internal_ws(size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  if (bytes > g_ws_bytes) {
+    if (g_ws) IRX_HIP(hipFree(g_ws));
+    g_ws = nullptr;
+    IRX_HIP(hipMalloc(&g_ws, bytes));
+    g_ws_bytes = bytes;
+  }
+  return g_ws;
+}
+
+bool eligible(const GemmArgs& a) {
+  if (a.dtype != BF16 || a.K % 64 != 0 || a.ldb % 8 != 0) return false;
+  if ((long)a.M * a.batch < 512) return false;     // tiny outputs: the 64x64 4-wave tiles waste less
+  if (a.geglu && (a.out_f32 || a.residual || a.batch != 1 || a.N % 128 != 0)) return false;
+  if (a.conv) return !a.out_f32 && a.g.C0 % 64 == 0 && a.g.C1 % 64 == 0;
+  return a.lda % 8 == 0 && (a.batch == 1 || a.sA % 8 == 0);
+}
+
+bool vec_ok(const GemmArgs& a) {
+  return !a.out_f32 && a.N % 8 == 0 && a.ldc % 8 == 0 && ((uintptr_t)a.C % 16) == 0 &&
+         (!a.residual || (a.ldr % 8 == 0 && ((uintptr_t)a.residual % 16) == 0)) &&
+         (a.batch == 1 || (a.sC % 8 == 0 && (!a.residual || a.sR % 8 == 0)));
+}
+
+}  // namespace
+
+bool gemm_geglu_fusable(const GemmArgs& a) {
+  if (!g_large_tiles || !a.geglu || !eligible(a) || !vec_ok(a)) return false;
+  return choose(a).BM != 0;
+}
+
+size_t gemm_workspace_bytes(const GemmArgs& a) {
+  if (!g_large_tiles || !eligible(a)) return 0;
+  const Choice c = choose(a);
+  if (c.BM == 0 || c.splits <= 1) return 0;
+  return (size_t)c.splits * a.batch * a.M * a.N * sizeof(float);
+}
+
+// Returns false (caller uses the 4-wave kernel) when the shape does not fit the large-tile path.
+bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
+  if (!eligible(a)) return false;
+  const Choice c = choose(a);
+  if (c.BM == 0) return false;
+  GemmArgs b = a;
+  b.vec_epilogue = vec_ok(a);
+  if (a.geglu && !b.vec_epilogue) return false;
+  Split sp;
+  sp.splits = c.splits;
+  sp.per = c.per;
+  if (c.splits > 1) {
+    if (!b.vec_epilogue && !a.out_f32) return false;     // reduce kernel needs 16-byte output rows
+    if (a.out_f32 && (a.ldc % 8 != 0 || a.N % 8 != 0)) return false;
+    const size_t need = (size_t)c.splits * a.batch * a.M * a.N * sizeof(float);
+    sp.ws = (a.splitk_ws && a.splitk_ws_bytes >= need) ? (float*)a.splitk_ws : internal_ws(need);
+  } else {
+    sp.per = a.K / 64;
+  }
+  switch (c.BM * 1000 + c.BN) {
+    case 256256: launch2<256, 256, 2, 4>(b, sp, s); break;
+    case 128320: launch2<128, 320, 2, 4>(b, sp, s); break;
+    case 256128: launch2<256, 128, 4, 2>(b, sp, s); break;
+    case 128256: launch2<128, 256, 2, 4>(b, sp, s); break;
+    case 128128: launch2<128, 128, 2, 4>(b, sp, s); break;
+    default: return false;
+  }
+  return true;
+}
+
+}  // namespace irx

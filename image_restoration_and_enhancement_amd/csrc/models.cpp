@@ -91,7 +91,6 @@ Act Model::new_act(Ctx& c, int n, int h, int w, int ch) {
 void Model::conv2d(Ctx& c, const Act& x0, const Act* x1, P w, P b, int cout, int k, int stride, int pad_t,
                    int pad_l, int hv, int wv, const Act& out, const float* rowadd, long rowadd_ld,
                    const void* residual, int out_f32, int ldc) {
-  if (c.ws->dry()) return;
   GemmArgs a;
   a.dtype = dt_;
   a.conv = 1;
@@ -109,12 +108,22 @@ void Model::conv2d(Ctx& c, const Act& x0, const Act* x1, P w, P b, int cout, int
   a.bias = b.set ? fptr(b) : nullptr;
   a.rowadd = rowadd; a.rowadd_ld = rowadd_ld; a.rows_per_group = out.h * out.w;
   a.residual = residual; a.ldr = a.ldc;
-  gemm(a, c.s);
+  run_gemm(c, a);
+}
+
+void Model::run_gemm(Ctx& c, GemmArgs& a) {
+  const size_t ws = gemm_workspace_bytes(a);     // split-K partials (shape-only decision)
+  void* p = ws ? c.ws->alloc(ws) : nullptr;
+  if (!c.ws->dry()) {
+    a.splitk_ws = p;
+    a.splitk_ws_bytes = ws;
+    gemm(a, c.s);
+  }
+  if (p) c.ws->free(p);
 }
 
 void Model::linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, const float* bias, void* C, long ldc,
                    int act, const void* residual, long ldr, int out_f32) {
-  if (c.ws->dry()) return;
   GemmArgs a;
   a.dtype = dt_;
   a.M = M; a.N = N; a.K = K;
@@ -125,7 +134,7 @@ void Model::linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, co
   a.act = act;
   a.residual = residual; a.ldr = ldr;
   a.out_f32 = out_f32;
-  gemm(a, c.s);
+  run_gemm(c, a);
 }
 
 void Model::gnorm(Ctx& c, const Act& x0, const Act* x1, P g, P b, float eps, int silu, const Act& out) {
@@ -181,7 +190,9 @@ Unet::XfW Unet::make_xf(const std::string& p, int c) {
   kv_names_.push_back(b + "attn2.to_v.weight");
   a.o2w = mat(b + "attn2.to_out.0.weight", c, c); a.o2b = vec(b + "attn2.to_out.0.bias", c);
   a.ln3w = vec(b + "norm3.weight", c); a.ln3b = vec(b + "norm3.bias", c);
-  a.ffw = mat(b + "ff.net.0.proj.weight", 8 * c, c); a.ffb = vec(b + "ff.net.0.proj.bias", 8 * c);
+  // GEGLU projection rows interleaved in (64 value, 64 gate) blocks so one output tile holds both halves
+  a.ffw = reg(b + "ff.net.0.proj.weight", IRX_LAYOUT_MAT_GEGLU64, dt_, {8 * c, c});
+  a.ffb = reg(b + "ff.net.0.proj.bias", IRX_LAYOUT_VEC_GEGLU64, F32, {8 * c});
   a.ff2w = mat(b + "ff.net.2.weight", c, 4 * c); a.ff2b = vec(b + "ff.net.2.bias", c);
   a.pow = mat(p + "proj_out.weight", c, c); a.pob = vec(p + "proj_out.bias", c);
   return a;
@@ -321,13 +332,24 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     attention(aa, c.s);
   }
   linear(c, n, C, M, C, a.o2w, C, fptr(a.o2b), h.p, C, ACT_NONE, h.p, C);
-  // GEGLU feed-forward
+  // GEGLU feed-forward: fused into the projection's epilogue when the large-tile path takes the shape
   lnorm(c, h.p, M, C, a.ln3w, a.ln3b, 1e-5f, n);
-  void* ff = c.ws->alloc(M * 8 * C * es);
-  linear(c, n, C, M, C, a.ffw, 8 * C, fptr(a.ffb), ff, 8 * C);
   void* g = c.ws->alloc(M * 4 * C * es);
-  if (!c.ws->dry()) geglu(dt_, ff, 8 * C, M, 4 * C, g, 4 * C, c.s);
-  c.ws->free(ff);
+  {
+    GemmArgs ga;
+    ga.dtype = dt_; ga.M = M; ga.N = 8 * C; ga.K = C;
+    ga.A = n; ga.lda = C; ga.B = ptr(a.ffw); ga.ldb = C;
+    ga.C = g; ga.ldc = 4 * C; ga.bias = fptr(a.ffb); ga.geglu = 1;
+    if (gemm_geglu_fusable(ga)) {
+      run_gemm(c, ga);
+    } else {
+      void* ff = c.ws->alloc(M * 8 * C * es);
+      ga.geglu = 0; ga.C = ff; ga.ldc = 8 * C;
+      run_gemm(c, ga);
+      if (!c.ws->dry()) geglu(dt_, ff, 8 * C, M, 4 * C, g, 4 * C, 1, c.s);
+      c.ws->free(ff);
+    }
+  }
   linear(c, g, 4 * C, M, 4 * C, a.ff2w, C, fptr(a.ff2b), h.p, C, ACT_NONE, h.p, C);
   c.ws->free(g);
   c.ws->free(att);

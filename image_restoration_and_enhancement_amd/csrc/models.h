@@ -72,6 +72,7 @@ class Model {
               const void* residual = nullptr, int out_f32 = 0, int ldc = -1);
   void linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, const float* bias, void* C, long ldc,
               int act = ACT_NONE, const void* residual = nullptr, long ldr = 0, int out_f32 = 0);
+  void run_gemm(Ctx& c, GemmArgs& a);   // allocates split-K partials from the workspace when needed
   void gnorm(Ctx& c, const Act& x0, const Act* x1, P g, P b, float eps, int silu, const Act& out);
   void lnorm(Ctx& c, const void* x, int rows, int C, P g, P b, float eps, void* out);
 

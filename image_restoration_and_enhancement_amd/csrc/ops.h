@@ -35,8 +35,17 @@ struct GemmArgs {
   float out_scale = 1.f;
   int act = ACT_NONE;     // applied after bias/rowadd, before residual
   int batch = 1;
+  int vec_epilogue = 0;   // set by the launcher: 16-byte LDS-staged output path is legal for this call
+  // GEGLU epilogue: B rows interleaved in (64 value, 64 gate) blocks (IRX_LAYOUT_*_GEGLU64); C gets N/2
+  // columns h * gelu(g).  Only the large-tile path fuses it (gemm_geglu_fusable); else see geglu().
+  int geglu = 0;
+  void* splitk_ws = nullptr; size_t splitk_ws_bytes = 0;   // caller workspace for split-K partials
 };
 void gemm(const GemmArgs& a, hipStream_t s);
+bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path; false if not eligible
+size_t gemm_workspace_bytes(const GemmArgs& a);           // split-K partial buffer the call will use
+bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can apply the GEGLU epilogue
+extern bool g_large_tiles;
 
 // ------------------------------------------------------------ normalisation
 // GroupNorm over NHWC (optionally a channel concat of two sources). Writes the normalised (and
@@ -63,7 +72,9 @@ struct AttnArgs {
 void attention(const AttnArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ elementwise / data movement
-void geglu(int dtype, const void* proj, long ldp, int M, int F, void* out, long ldo, hipStream_t s);
+// out[m][f] = h * gelu_erf(g): h = proj[m][f], g = proj[m][F + f]; with interleave64 the proj columns are
+// (64 value, 64 gate) block pairs (the GEGLU64 weight layout the fused epilogue uses)
+void geglu(int dtype, const void* proj, long ldp, int M, int F, void* out, long ldo, int interleave64, hipStream_t s);
 void timestep_embed(int dtype, const float* t, int B, int dim, int flip_sin_to_cos, float shift, void* out,
                     hipStream_t s);
 void embed_tokens(int dtype, const int* ids, int B, int L, const void* tok, const void* pos, int D, void* out,

@@ -79,12 +79,22 @@ class ParamSpec:
     nbytes: int
 
 
+def geglu64_order(n: int) -> torch.Tensor:
+    """Source row of each packed row for the GEGLU64 layout ([values; gates] -> (64 v, 64 g) pairs)."""
+    r = torch.arange(n)
+    return (r // 128) * 64 + r % 64 + (r % 128 >= 64).long() * (n // 2)
+
+
 def _convert(t: torch.Tensor, layout: int) -> torch.Tensor:
     t = t.detach().float()
     if layout == L.IRX_LAYOUT_VEC:
         return t.reshape(-1)
     if layout == L.IRX_LAYOUT_MAT:
         return t.reshape(t.shape[0], -1)
+    if layout == L.IRX_LAYOUT_VEC_GEGLU64:
+        return t.reshape(-1)[geglu64_order(t.numel())]
+    if layout == L.IRX_LAYOUT_MAT_GEGLU64:
+        return t.reshape(t.shape[0], -1)[geglu64_order(t.shape[0])]
     if layout == L.IRX_LAYOUT_CONV:
         return t.permute(0, 2, 3, 1)          # OIHW -> O,KH,KW,I
     return t

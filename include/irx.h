@@ -34,6 +34,10 @@ extern "C" {
 #define IRX_LAYOUT_MAT 1   /* [N][K] from [N][K] or [N][K][1][1], zero padded         */
 #define IRX_LAYOUT_CONV 2  /* [Cout][KH][KW][Cin] from OIHW, zero padded on Cout/Cin   */
 #define IRX_LAYOUT_EMB 3   /* [rows][D] embedding table                                */
+/* GEGLU projection (diffusers ff.net.0.proj, rows [values; gates]) re-ordered into (64 value rows,
+ * 64 gate rows) block pairs: packed row r <- source row (r/128)*64 + r%64 (+ N/2 if r%128 >= 64) */
+#define IRX_LAYOUT_MAT_GEGLU64 4
+#define IRX_LAYOUT_VEC_GEGLU64 5
 
 typedef struct irx_model irx_model;
 
@@ -68,6 +72,9 @@ typedef struct {
 
 const char* irx_last_error(void);
 int irx_version(void);
+
+/* engine options: "large_tiles" (1 = 8-wave LDS-DMA GEMM/conv path where eligible, 0 = 4-wave kernel) */
+int irx_set_option(const char* name, int value);
 
 /* ---- optional per-launch HIP-event timing of the MFMA kernels (bench.py roofline) ---- */
 int irx_profile_begin(void);
@@ -151,6 +158,9 @@ int irx_op_attention(void* stream, int dtype, int batch, int heads, int lq, int 
                      long sq, const void* k, long ldk, long sk, const void* v, long ldv, long sv, void* o, long ldo,
                      long so, float scale, int causal);
 int irx_op_geglu(void* stream, int dtype, const void* proj, int M, int F, void* out);
+/* C[M][N/2] = GEGLU(A B^T + bias) with B/bias in the GEGLU64 row order (fused epilogue, bf16 large tiles) */
+int irx_op_gemm_geglu(void* stream, int dtype, int M, int N, int K, const void* A, const void* B, const float* bias,
+                      void* C);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Per-shape micro-benchmark of the MFMA conv/GEMM/attention kernels at the UNet's batch-16 (CFG x 8
+images) 512x512 shapes.  Times each op with HIP events over N iterations (interleaved variants in
+one process) and prints TF/s.  Usage: python scripts/kbench.py [--iters 20] [--only conv|gemm|attn]
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from image_restoration_and_enhancement_amd import _lib as L  # noqa: E402
+from tests import opref as O  # noqa: E402
+
+CONVS = [  # (label, N, H, W, C0, C1, Cout, k, stride, up)
+    ("conv320@64", 16, 64, 64, 320, 0, 320, 3, 1, None),
+    ("conv640@32", 16, 32, 32, 640, 0, 640, 3, 1, None),
+    ("conv1280@16", 16, 16, 16, 1280, 0, 1280, 3, 1, None),
+    ("conv1280@8", 16, 8, 8, 1280, 0, 1280, 3, 1, None),
+    ("cat1280+640->640@32", 16, 32, 32, 1280, 640, 640, 3, 1, None),
+    ("up1280@16->32", 16, 16, 16, 1280, 0, 1280, 3, 1, (32, 32)),
+    ("vae512@128", 8, 128, 128, 512, 0, 512, 3, 1, None),
+    ("vae256@256", 8, 256, 256, 256, 0, 256, 3, 1, None),
+    ("vae128@512", 8, 512, 512, 128, 0, 128, 3, 1, None),
+]
+GEMMS = [  # (label, M, N, K)
+    ("lin320x320@64", 65536, 320, 320),
+    ("qkv@64", 65536, 960, 320),
+    ("ff1@64", 65536, 2560, 320),
+    ("ff2@64", 65536, 320, 1280),
+    ("lin640@32", 16384, 640, 640),
+    ("ff1@32", 16384, 5120, 640),
+    ("ff2@32", 16384, 640, 2560),
+    ("lin1280@16", 4096, 1280, 1280),
+    ("ff1@16", 4096, 10240, 1280),
+]
+ATTNS = [  # (label, B, L, Lk, C)
+    ("self d40 L4096", 16, 4096, 4096, 320),
+    ("self d80 L1024", 16, 1024, 1024, 640),
+    ("self d160 L256", 16, 256, 256, 1280),
+    ("cross d40", 16, 4096, 77, 320),
+]
+
+
+def timeit(fn, iters):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    L.load()
+    dt = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    variants = [("large", 1), ("4wave", 0)]
+    if args.only in ("", "conv"):
+        for lab, N, H, W, C0, C1, Co, k, s, up in CONVS:
+            x0 = torch.randn(N, H, W, C0, device=dev, generator=g).to(dt)
+            x1 = torch.randn(N, H, W, C1, device=dev, generator=g).to(dt) if C1 else None
+            w = (torch.randn(Co, C0 + C1, k, k, device=dev, generator=g) / math.sqrt((C0 + C1) * k * k)).to(dt)
+            b = torch.zeros(Co, device=dev)
+            Ho, Wo = up if up else (H, W)
+            flops = 2.0 * N * Ho * Wo * Co * (C0 + C1) * k * k
+            res = []
+            for vn, v in variants:
+                L.call("irx_set_option", b"large_tiles", v)
+                ms = timeit(lambda: O.conv2d(x0, w, b, x1=x1, up_hw=up), args.iters)
+                res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
+            print(f"{lab:24s} " + " | ".join(res), flush=True)
+    if args.only in ("", "gemm"):
+        for lab, M, N, K in GEMMS:
+            A = torch.randn(M, K, device=dev, generator=g).to(dt)
+            Bw = (torch.randn(N, K, device=dev, generator=g) / math.sqrt(K)).to(dt)
+            flops = 2.0 * M * N * K
+            res = []
+            for vn, v in variants:
+                L.call("irx_set_option", b"large_tiles", v)
+                ms = timeit(lambda: O.gemm(A, Bw), args.iters)
+                res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
+            print(f"{lab:24s} " + " | ".join(res), flush=True)
+    L.call("irx_set_option", b"large_tiles", 1)
+    if args.only in ("", "attn"):
+        for lab, B, Lq, Lk, C in ATTNS:
+            q = torch.randn(B, Lq, C, device=dev, generator=g).to(dt)
+            k = torch.randn(B, Lk, C, device=dev, generator=g).to(dt)
+            v = torch.randn(B, Lk, C, device=dev, generator=g).to(dt)
+            flops = 4.0 * B * Lq * Lk * C
+            ms = timeit(lambda: O.attention(q, k, v, 8), args.iters)
+            print(f"{lab:24s} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF", flush=True)
+
+
+if __name__ == "__main__":
+    main()

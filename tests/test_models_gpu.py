@@ -50,8 +50,9 @@ def test_clip(device, denoise_sd, dtype, tol):
     assert err < tol, err
 
 
-@pytest.mark.parametrize("dtype,tol", [("fp32", 2e-4), ("bf16", 4e-2)])
-@pytest.mark.parametrize("h,w", [(8, 8), (7, 5)])
+@pytest.mark.parametrize("dtype,tol,h,w", [("fp32", 2e-4, 8, 8), ("fp32", 2e-4, 7, 5), ("bf16", 4e-2, 8, 8),
+                                           ("bf16", 4e-2, 7, 5),
+                                           ("bf16", 4e-2, 32, 32)])   # large-tile / fused-GEGLU kernels
 def test_unet(device, denoise_sd, dtype, tol, h, w):
     pc, sd = denoise_sd
     unet = UNet(pc.unet, dtype, device)
@@ -162,7 +163,8 @@ def test_inpaint_pipeline_fp32(device):
 
 
 def test_batch_shares_noise(device):
-    """Every image of a batch equals the same image run alone (per-call reseed semantics)."""
+    """Every image of a batch equals the same image run alone (per-call reseed semantics).  Batch size
+    can change the bf16 GEMM tile / split-K choice (summation order), so equality is up to 2 uint8 levels."""
     prompt, strength, steps, guidance = PR.TASKS["denoise"]
     pc, sd = MC.state_dicts("denoise")
     eng = SDEngine(pc, "bf16", device, state_dicts=sd)
@@ -172,4 +174,4 @@ def test_batch_shares_noise(device):
     for i in range(3):
         one = eng.img2img(torch.from_numpy(imgs[i:i + 1]).to(device).contiguous(), prompt, strength, steps,
                           guidance, n_evals=2).images_u8.cpu()
-        assert torch.equal(one[0], batch[i])
+        assert (one[0].int() - batch[i].int()).abs().max() <= 2

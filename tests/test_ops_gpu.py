@@ -206,3 +206,79 @@ def test_geglu(device, dt):
     h, g = _q(x, dt).chunk(2, dim=-1)
     ref = h * F.gelu(g)
     assert O.rel_err(got, ref) < TOL[dt]
+
+
+# ------------------------------------------------------------------ large-tile (8-wave LDS-DMA) path
+@pytest.fixture(params=[1, 0], ids=["large_tiles", "4wave"])
+def tiles(request):
+    from image_restoration_and_enhancement_amd import _lib as L
+    L.call("irx_set_option", b"large_tiles", request.param)
+    yield request.param
+    L.call("irx_set_option", b"large_tiles", 1)
+
+
+@pytest.mark.parametrize("case", [
+    # (N, Hin, Win, C0, C1, Cout, k, stride, pad, up_hw)
+    (2, 64, 64, 320, 0, 320, 3, 1, 1, None),        # level-0 resnet conv  -> 128x320 tile
+    (4, 32, 32, 1280, 640, 640, 3, 1, 1, None),     # up-block concat conv -> 128x320 tile
+    (4, 16, 16, 1280, 0, 1280, 3, 1, 1, (32, 32)),  # Upsample2D conv      -> 256x256 tile
+    (2, 63, 41, 256, 0, 512, 3, 2, 1, None),        # odd sizes, stride 2  -> 256x256 tile
+    (3, 40, 40, 128, 128, 128, 1, 1, 0, None),      # 1x1 concat shortcut  -> 256x128 tile
+])
+def test_conv_large(device, tiles, case):
+    dt = torch.bfloat16
+    N, H, W, C0, C1, Co, k, s, p, up = case
+    x0 = _r(N, C0, H, W, seed=70)
+    x1 = _r(N, C1, H, W, seed=71) if C1 else None
+    w = _r(Co, C0 + C1, k, k, seed=72, scale=1 / math.sqrt((C0 + C1) * k * k))
+    b = _r(Co, seed=73)
+    res = None
+    got = O.conv2d(_dev(x0.permute(0, 2, 3, 1), dt, device), w.to(dt).float(), b, stride=s, pad=(p, p),
+                   x1=_dev(x1.permute(0, 2, 3, 1), dt, device) if C1 else None, up_hw=up)
+    xin = torch.cat([_q(x0, dt)] + ([_q(x1, dt)] if C1 else []), 1)
+    if up is not None:
+        xin = F.interpolate(xin, size=up, mode="nearest")
+    ref = F.conv2d(xin, _q(w, dt), b, stride=s, padding=p).permute(0, 2, 3, 1)
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("M,N,K,res,f32", [(8192, 2560, 320, False, False), (4096, 320, 1280, True, False),
+                                           (5000, 640, 640, True, True), (4096, 512, 512, False, False),
+                                           (6144, 384, 128, False, True)])
+def test_gemm_large(device, tiles, M, N, K, res, f32):
+    dt = torch.bfloat16
+    A = _r(M, K, seed=74)
+    Bw = _r(N, K, seed=75, scale=1 / math.sqrt(K))
+    bias = _r(N, seed=76)
+    R = _r(M, N, seed=77) if res else None
+    got = O.gemm(_dev(A, dt, device), _dev(Bw, dt, device), bias=bias.to(device),
+                 residual=_dev(R, dt, device) if res else None, out_f32=f32)
+    ref = _q(A, dt) @ _q(Bw, dt).T + bias + (_q(R, dt) if res else 0)
+    assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("M,C", [(8192, 320), (4096, 640)])
+def test_gemm_geglu_fused(device, M, C):
+    """ff.net.0.proj + GEGLU in one kernel (GEGLU64 weight order) vs Linear -> chunk -> h * gelu(g)."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    from image_restoration_and_enhancement_amd.engine import geglu64_order
+    dt = torch.bfloat16
+    A = _r(M, C, seed=80)
+    Wt = _r(8 * C, C, seed=81, scale=1 / math.sqrt(C))
+    bias = _r(8 * C, seed=82)
+    perm = geglu64_order(8 * C)
+    out = torch.empty(M, 4 * C, dtype=dt, device=device)
+    a_d, w_d, b_d = _dev(A, dt, device), _dev(Wt[perm], dt, device), bias[perm].to(device).contiguous()
+    L.call("irx_op_gemm_geglu", O.S(), L.IRX_BF16, M, 8 * C, C, O.P(a_d), O.P(w_d), O.P(b_d), O.P(out))
+    pr = _q(A, dt) @ _q(Wt, dt).T + bias
+    h, g = pr.chunk(2, dim=-1)
+    assert O.rel_err(out, h * F.gelu(g)) < TOL[dt]
+
+
+def test_gemm_large_batched(device, tiles):
+    dt = torch.bfloat16
+    b, M, N, K = 2, 4096, 256, 512
+    A, Bw = _r(b, M, K, seed=78), _r(b, N, K, seed=79, scale=0.05)
+    got = O.gemm(_dev(A, dt, device), _dev(Bw, dt, device), batch=b, out_f32=True)
+    ref = torch.bmm(_q(A, dt), _q(Bw, dt).transpose(1, 2))
+    assert O.rel_err(got, ref) < TOL[dt]
