@@ -280,6 +280,208 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// bf16 throughput kernel: v_mfma_f32_16x16x32_bf16 for both products.
+//   S^T = K Q^T : K fragments by ds_read_b128 (d padded to DQ, a multiple of 32), Q^T in registers.
+//   O^T += V^T P^T over 32-key chunks: P^T is the exponentiated S^T accumulator of two 16-key tiles
+//   (lane group g holds keys 4g..4g+3 of each), V^T comes from two ds_read_b64_tr_b16 of the same
+//   key sets, so the permuted k order matches on both operands.
+// KT keys per LDS tile (128 at d <= 80, 64 at d = 160 to bound registers); 4 waves x 32 queries.
+template <int DQ, int DV, int KT>
+__global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
+  constexpr int SK = DQ + 8;                                     // 16 rows x b128 reads conflict-free
+  constexpr int SV = ((DV * 2 / 32) % 2 == 1) ? DV : DV + 16;    // 8 rows x 32 B tr reads conflict-free
+  constexpr int NDC = DQ / 32, NDT = DV / 16, NKT = KT / 16, NKC = KT / 32;
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[KT * SK];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[KT * SV];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int qb0 = blockIdx.x * kQB;
+  const int q0 = qb0 + wave * (kQT * 16);
+  const int d = a.d;
+  const bf16_t* __restrict__ Q = (const bf16_t*)a.q + (long)b * a.sq + (long)h * d;
+  const bf16_t* __restrict__ K = (const bf16_t*)a.k + (long)b * a.sk + (long)h * d;
+  const bf16_t* __restrict__ V = (const bf16_t*)a.v + (long)b * a.sv + (long)h * d;
+
+  for (int i = tid; i < KT * SK; i += 256) Ks[i] = 0;
+  for (int i = tid; i < KT * SV; i += 256) Vs[i] = 0;
+
+  s16x8 qf[kQT][NDC];
+#pragma unroll
+  for (int qt = 0; qt < kQT; ++qt) {
+    const int q = q0 + qt * 16 + li;
+#pragma unroll
+    for (int dc = 0; dc < NDC; ++dc) {
+      const int e = dc * 32 + 8 * g;
+      s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (q < a.Lq && e < d) v = *(const s16x8*)(Q + (long)q * a.ldq + e);
+      qf[qt][dc] = v;
+    }
+  }
+  f32x4 o[NDT][kQT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int j = 0; j < kQT; ++j) o[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrow[kQT], lrow[kQT];
+#pragma unroll
+  for (int j = 0; j < kQT; ++j) { mrow[j] = -INFINITY; lrow[j] = 0.f; }
+
+  const float sl2 = a.scale * 1.4426950408889634f;
+  int kend = a.Lk;
+  if (a.causal) kend = min(kend, qb0 + kQB);
+  const int cpr = d / 8;                                   // 16-byte chunks per K/V row
+  constexpr int NCH = (KT * (DV / 8) + 255) / 256;       // d <= DV
+  uint4 kreg[NCH], vreg[NCH];
+  auto load_regs = [&](int j0) {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = tid + 256 * u;
+      kreg[u] = make_uint4(0, 0, 0, 0);
+      vreg[u] = make_uint4(0, 0, 0, 0);
+      if (idx < KT * cpr) {
+        const int r = idx / cpr, c = idx - r * cpr;
+        if (j0 + r < a.Lk) {
+          kreg[u] = *(const uint4*)(K + (long)(j0 + r) * a.ldk + c * 8);
+          vreg[u] = *(const uint4*)(V + (long)(j0 + r) * a.ldv + c * 8);
+        }
+      }
+    }
+  };
+  load_regs(0);
+
+  for (int j0 = 0; j0 < kend; j0 += KT) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = tid + 256 * u;
+      if (idx < KT * cpr) {
+        const int r = idx / cpr, c = idx - r * cpr;
+        *(uint4*)(Ks + r * SK + c * 8) = kreg[u];
+        uint2* pv = (uint2*)(Vs + r * SV + c * 8);
+        pv[0] = make_uint2(vreg[u].x, vreg[u].y);
+        pv[1] = make_uint2(vreg[u].z, vreg[u].w);
+      }
+    }
+    __syncthreads();
+    if (j0 + KT < kend) load_regs(j0 + KT);
+
+    f32x4 s[NKT][kQT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int qt = 0; qt < kQT; ++qt) s[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dc = 0; dc < NDC; ++dc) {
+        const s16x8 kf = *(const s16x8*)(Ks + (kt * 16 + li) * SK + dc * 32 + 8 * g);
+#pragma unroll
+        for (int qt = 0; qt < kQT; ++qt)
+          s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf),
+                                                              __builtin_bit_cast(bf16x8, qf[qt][dc]), s[kt][qt], 0, 0, 0);
+      }
+    }
+
+    const bool need_mask = (j0 + KT > a.Lk) || (a.causal && j0 + KT - 1 > q0);
+    float nbq[kQT];
+#pragma unroll
+    for (int qt = 0; qt < kQT; ++qt) {
+      const int q = q0 + qt * 16 + li;
+      if (need_mask) {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = j0 + kt * 16 + 4 * g + i;
+            if (key >= a.Lk || (a.causal && key > q)) s[kt][qt][i] = -INFINITY;
+          }
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+        tmax = fmaxf(tmax, fmaxf(fmaxf(s[kt][qt][0], s[kt][qt][1]), fmaxf(s[kt][qt][2], s[kt][qt][3])));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      const float mnew = fmaxf(mrow[qt], tmax);
+      const bool none = mnew == -INFINITY;
+      const float alpha = none ? 1.f : exp2f((mrow[qt] - mnew) * sl2);
+      nbq[qt] = none ? 0.f : -mnew * sl2;
+      mrow[qt] = mnew;
+      lrow[qt] *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt][qt] *= alpha;
+    }
+
+    // per 32-key chunk: exponentiate into the B operand, then its PV MFMAs (keeps 1 chunk of P live)
+#pragma unroll
+    for (int c = 0; c < NKC; ++c) {
+      s16x8 pf[kQT];
+#pragma unroll
+      for (int qt = 0; qt < kQT; ++qt) {
+        float lsum = 0.f;
+#pragma unroll
+        for (int half = 0; half < 2; ++half)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = exp2f(fmaf(s[2 * c + half][qt][i], sl2, nbq[qt]));
+            lsum += p;
+            pf[qt][half * 4 + i] = (short)f2bf(p);
+          }
+        lrow[qt] += lsum;
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const bf16_t* v1 = Vs + (c * 32 + 4 * g + (li >> 2)) * SV + dt * 16 + 4 * (li & 3);
+        const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)v1);
+        const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v1 + 16 * SV));
+        const s16x8 vf = {t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+#pragma unroll
+        for (int qt = 0; qt < kQT; ++qt)
+          o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vf),
+                                                              __builtin_bit_cast(bf16x8, pf[qt]), o[dt][qt], 0, 0, 0);
+      }
+    }
+  }
+
+  bf16_t* __restrict__ O = (bf16_t*)a.o + (long)b * a.so + (long)h * d;
+#pragma unroll
+  for (int qt = 0; qt < kQT; ++qt) {
+    float l = lrow[qt];
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int q = q0 + qt * 16 + li;
+    if (q >= a.Lq) continue;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const int e = dt * 16 + 4 * g;
+      if (e >= d) continue;
+      s16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (short)f2bf(o[dt][qt][i] * inv);
+      *(s16x4*)(O + (long)q * a.ldo + e) = v;
+    }
+  }
+}
+
+void launch_bf16(const AttnArgs& a, hipStream_t s) {
+  dim3 grid((a.Lq + kQB - 1) / kQB, a.H, a.B), block(256);
+  const int dq = (a.d + 31) / 32 * 32;
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn2_kernel<") + std::to_string(dq) + ">"
+                         : std::string(),
+               4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
+  switch (a.d) {
+    case 40: attn2_kernel<64, 48, 128><<<grid, block, 0, s>>>(a); break;
+    case 64: attn2_kernel<64, 64, 128><<<grid, block, 0, s>>>(a); break;
+    case 80: attn2_kernel<96, 80, 64><<<grid, block, 0, s>>>(a); break;
+    case 160: attn2_kernel<160, 160, 32><<<grid, block, 0, s>>>(a); break;
+    default: throw Error("attention: unsupported head dim " + std::to_string(a.d));
+  }
+  IRX_LAUNCH_CHECK();
+}
+
 template <typename T>
 void launch_t(const AttnArgs& a, hipStream_t s) {
   dim3 grid((a.Lq + kQB - 1) / kQB, a.H, a.B), block(256);
@@ -308,7 +510,10 @@ void attention(const AttnArgs& a, hipStream_t s) {
   IRX_CHECK((a.ldq * es) % 8 == 0 && (a.ldo * es) % 8 == 0, "Q/O rows must be 8-byte aligned");
   IRX_CHECK(((uintptr_t)a.k % 16) == 0 && ((uintptr_t)a.v % 16) == 0, "K/V base alignment");
   if (a.dtype == F32) launch_t<float>(a, s);
+  else if (g_attn_v2 && a.d % 8 == 0 && (a.ldq % 8) == 0 && ((uintptr_t)a.q % 16) == 0) launch_bf16(a, s);
   else launch_t<bf16_t>(a, s);
 }
+
+bool g_attn_v2 = true;
 
 }  // namespace irx

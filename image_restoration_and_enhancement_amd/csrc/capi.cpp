@@ -58,6 +58,7 @@ int irx_set_option(const char* name, int value) {
   IRX_CHECK(name, "null option name");
   const std::string n(name);
   if (n == "large_tiles") g_large_tiles = value != 0;
+  else if (n == "attn_v2") g_attn_v2 = value != 0;
   else throw Error("unknown option " + n);
   IRX_API_END
 }

@@ -12,20 +12,21 @@
 namespace irx {
 namespace {
 
-constexpr int kPix = 64;   // pixels per stats chunk
+constexpr int kMaxChunks = 256;   // stats blocks per image (pixels per chunk grows with the image)
 
-size_t n_chunks(int HW) { return (HW + kPix - 1) / kPix; }
+int n_chunks(int HW) { return std::min((HW + 63) / 64, kMaxChunks); }
+int chunk_pix(int HW) { const int n = n_chunks(HW); return (HW + n - 1) / n; }
 
 template <typename T>
 __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x0, const T* __restrict__ x1,
-                                                       int C0, int C1, int HW, int G, double* part) {
+                                                       int C0, int C1, int HW, int G, int cpix, double* part) {
   constexpr int VEC = 16 / (int)sizeof(T);
   __shared__ double gs[64], gq[64];
   const int C = C0 + C1;
   const int nv = C / VEC;                      // vectors per pixel
   const int cg = C / G;
   const int n = blockIdx.y, chunk = blockIdx.x;
-  const int p0 = chunk * kPix, p1 = min(HW, p0 + kPix);
+  const int p0 = chunk * cpix, p1 = min(HW, p0 + cpix);
   if (threadIdx.x < 64) { gs[threadIdx.x] = 0.0; gq[threadIdx.x] = 0.0; }
   __syncthreads();
   // thread -> (vector v, pixel lane r); each thread owns up to 2 vectors (C <= 4096)
@@ -34,24 +35,39 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x0,
   for (int vb = 0; vb < nv; vb += 256) {
     const int v = vb + (nv >= 256 ? threadIdx.x : threadIdx.x % nv);
     if (v >= nv || r >= rows) continue;
-    double s[VEC], q[VEC];
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) { s[e] = 0.0; q[e] = 0.0; }
+    // fp32 sums of (x - x0), x0 = this thread's first sample per channel (keeps the fp32 partials free of
+    // mean^2 cancellation); re-expanded to raw sum / sum of squares in fp64 for the cross-thread merge
+    float s[VEC], q[VEC], x0v[VEC];
     const int c = v * VEC;
     const T* src = c < C0 ? x0 + c : x1 + (c - C0);
     const int ld = c < C0 ? C0 : C1;
+    int cnt = 0;
+    if (p0 + r < p1) {
+      Vec16<T>::unpack(*(const uint4*)(src + ((long)n * HW + p0 + r) * ld), x0v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) x0v[e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) { s[e] = 0.f; q[e] = 0.f; }
     for (int p = p0 + r; p < p1; p += rows) {
       const uint4 u = *(const uint4*)(src + ((long)n * HW + p) * ld);
       float f[VEC];
       Vec16<T>::unpack(u, f);
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) { s[e] += f[e]; q[e] += (double)f[e] * f[e]; }
+      for (int e = 0; e < VEC; ++e) {
+        const float dv = f[e] - x0v[e];
+        s[e] += dv;
+        q[e] = fmaf(dv, dv, q[e]);
+      }
+      ++cnt;
     }
 #pragma unroll
     for (int e = 0; e < VEC; ++e) {
       const int grp = (c + e) / cg;
-      atomicAdd(&gs[grp], s[e]);
-      atomicAdd(&gq[grp], q[e]);
+      const double xs = x0v[e], ds = s[e];
+      atomicAdd(&gs[grp], cnt * xs + ds);
+      atomicAdd(&gq[grp], cnt * xs * xs + 2.0 * xs * ds + (double)q[e]);
     }
   }
   __syncthreads();
@@ -62,10 +78,24 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x0,
   }
 }
 
+// per (image, group): fold the chunk partials into (mean, rstd) once
+__global__ __launch_bounds__(64) void gn_finalize_kernel(const double* __restrict__ part, int nchunk, int G,
+                                                         double cnt, float eps, float2* __restrict__ mr) {
+  const int n = blockIdx.x, g = threadIdx.x;
+  if (g >= G) return;
+  double s = 0.0, q = 0.0;
+  const double* p = part + ((long)n * nchunk) * G * 2 + g * 2;
+  for (int c = 0; c < nchunk; ++c) { s += p[(long)c * G * 2]; q += p[(long)c * G * 2 + 1]; }
+  const double mean = s / cnt;
+  double var = q / cnt - mean * mean;
+  if (var < 0.0) var = 0.0;
+  mr[n * G + g] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x0, const T* __restrict__ x1, int C0,
-                                                       int C1, int HW, int G, int nchunk, const double* part,
-                                                       float eps, const float* __restrict__ gamma,
+                                                       int C1, int HW, int G, const float2* __restrict__ mr,
+                                                       const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, int silu, T* __restrict__ out,
                                                        int pix_per_block) {
   constexpr int VEC = 16 / (int)sizeof(T);
@@ -74,15 +104,9 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x0,
   const int C = C0 + C1;
   const int n = blockIdx.y;
   if (threadIdx.x < G) {
-    double s = 0.0, q = 0.0;
-    const double* p = part + ((long)n * nchunk) * G * 2 + threadIdx.x * 2;
-    for (int c = 0; c < nchunk; ++c) { s += p[(long)c * G * 2]; q += p[(long)c * G * 2 + 1]; }
-    const double cnt = (double)HW * (C / G);
-    const double mean = s / cnt;
-    double var = q / cnt - mean * mean;
-    if (var < 0.0) var = 0.0;
-    mean_s[threadIdx.x] = (float)mean;
-    rstd_s[threadIdx.x] = (float)(1.0 / sqrt(var + (double)eps));
+    const float2 v = mr[n * G + threadIdx.x];
+    mean_s[threadIdx.x] = v.x;
+    rstd_s[threadIdx.x] = v.y;
   }
   __syncthreads();
   const int cg = C / G;
@@ -93,21 +117,32 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x0,
     ab[C + c] = beta[c] - mean_s[grp] * sc;
   }
   __syncthreads();
+  // thread -> fixed 16-byte channel chunk (its scale/shift held in registers) x a pixel stride
   const int nv = C / VEC;
+  const int rows = nv >= (int)blockDim.x ? 1 : blockDim.x / nv;
+  const int r = threadIdx.x / (nv >= (int)blockDim.x ? blockDim.x : nv);
   const int p0 = blockIdx.x * pix_per_block;
-  const int total = min(pix_per_block, HW - p0) * nv;
-  for (int i = threadIdx.x; i < total; i += blockDim.x) {
-    const long p = p0 + i / nv;
-    const int c = (i % nv) * VEC;
-    const T* src = c < C0 ? x0 + ((long)n * HW + p) * C0 + c : x1 + ((long)n * HW + p) * C1 + (c - C0);
-    float f[VEC];
-    Vec16<T>::unpack(*(const uint4*)src, f);
+  const int p1 = min(HW, p0 + pix_per_block);
+  for (int vb = 0; vb < nv; vb += blockDim.x) {
+    const int v = vb + (nv >= (int)blockDim.x ? threadIdx.x : threadIdx.x % nv);
+    if (v >= nv || r >= rows) continue;
+    const int c = v * VEC;
+    float sc[VEC], sh[VEC];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      float y = f[e] * ab[c + e] + ab[C + c + e];
-      f[e] = silu ? silu_f(y) : y;
+    for (int e = 0; e < VEC; ++e) { sc[e] = ab[c + e]; sh[e] = ab[C + c + e]; }
+    const T* src = c < C0 ? x0 + (long)n * HW * C0 + c : x1 + (long)n * HW * C1 + (c - C0);
+    const int ld = c < C0 ? C0 : C1;
+    T* dst = out + (long)n * HW * C + c;
+    for (int p = p0 + r; p < p1; p += rows) {
+      float f[VEC];
+      Vec16<T>::unpack(*(const uint4*)(src + (long)p * ld), f);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float y = fmaf(f[e], sc[e], sh[e]);
+        f[e] = silu ? y * __builtin_amdgcn_rcpf(1.0f + __expf(-y)) : y;
+      }
+      *(uint4*)(dst + (long)p * C) = Vec16<T>::pack(f);
     }
-    *(uint4*)(out + ((long)n * HW + p) * C + c) = Vec16<T>::pack(f);
   }
 }
 
@@ -165,15 +200,21 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long l
 template <typename T>
 void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps, const float* gamma,
           const float* beta, int silu, void* out, void* ws, hipStream_t s) {
-  const int nch = (int)n_chunks(HW);
-  gn_stats_kernel<T><<<dim3(nch, N), 256, 0, s>>>((const T*)x0, (const T*)x1, C0, C1, HW, G, (double*)ws);
-  IRX_LAUNCH_CHECK();
+  const int nch = n_chunks(HW);
+  double* part = (double*)ws;
+  float2* mr = (float2*)(part + (size_t)N * nch * G * 2);
   const int C = C0 + C1;
+  gn_stats_kernel<T><<<dim3(nch, N), 256, 0, s>>>((const T*)x0, (const T*)x1, C0, C1, HW, G, chunk_pix(HW), part);
+  IRX_LAUNCH_CHECK();
+  gn_finalize_kernel<<<N, 64, 0, s>>>(part, nch, G, (double)HW * (C / G), eps, mr);
+  IRX_LAUNCH_CHECK();
   const int VEC = 16 / (int)sizeof(T);
-  // ~16 vectors per thread per block
-  int ppb = max(1, (256 * 16) / (C / VEC));
+  // ~16 pixels per thread per block, one fixed channel chunk per thread
+  const int nv = C / VEC;
+  const int rows = nv >= 256 ? 1 : 256 / nv;
+  const int ppb = rows * 16;
   gn_apply_kernel<T><<<dim3((HW + ppb - 1) / ppb, N), 256, 2 * C * sizeof(float), s>>>(
-      (const T*)x0, (const T*)x1, C0, C1, HW, G, nch, (const double*)ws, eps, gamma, beta, silu, (T*)out, ppb);
+      (const T*)x0, (const T*)x1, C0, C1, HW, G, mr, gamma, beta, silu, (T*)out, ppb);
   IRX_LAUNCH_CHECK();
 }
 
@@ -193,7 +234,9 @@ void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamm
 
 }  // namespace
 
-size_t gn_ws_bytes(int N, int HW, int G) { return (size_t)N * n_chunks(HW) * G * 2 * sizeof(double); }
+size_t gn_ws_bytes(int N, int HW, int G) {
+  return (size_t)N * n_chunks(HW) * G * 2 * sizeof(double) + (size_t)N * G * sizeof(float2);
+}
 
 void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
                 const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s) {

@@ -101,8 +101,13 @@ def main():
             k = torch.randn(B, Lk, C, device=dev, generator=g).to(dt)
             v = torch.randn(B, Lk, C, device=dev, generator=g).to(dt)
             flops = 4.0 * B * Lq * Lk * C
-            ms = timeit(lambda: O.attention(q, k, v, 8), args.iters)
-            print(f"{lab:24s} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF", flush=True)
+            res = []
+            for vn, v2 in (("v2", 1), ("v1", 0)):
+                L.call("irx_set_option", b"attn_v2", v2)
+                ms = timeit(lambda: O.attention(q, k, v, 8), args.iters)
+                res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
+            L.call("irx_set_option", b"attn_v2", 1)
+            print(f"{lab:24s} " + " | ".join(res), flush=True)
 
 
 if __name__ == "__main__":

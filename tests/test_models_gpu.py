@@ -163,15 +163,16 @@ def test_inpaint_pipeline_fp32(device):
 
 
 def test_batch_shares_noise(device):
-    """Every image of a batch equals the same image run alone (per-call reseed semantics).  Batch size
-    can change the bf16 GEMM tile / split-K choice (summation order), so equality is up to 2 uint8 levels."""
+    """Every image of a batch equals the same image run alone (per-call reseed semantics).  fp32 engine:
+    bit-exact (per-element K order never depends on the batch).  (bf16 large-tile GEMMs may pick another
+    tile / split-K for another batch size, which changes summation order — not asserted bitwise.)"""
     prompt, strength, steps, guidance = PR.TASKS["denoise"]
     pc, sd = MC.state_dicts("denoise")
-    eng = SDEngine(pc, "bf16", device, state_dicts=sd)
+    eng = SDEngine(pc, "fp32", device, state_dicts=sd)
     imgs = np.stack([MC.smooth_image(64, 64, seed=s) for s in (1, 2, 3)])
     batch = eng.img2img(torch.from_numpy(imgs).to(device).contiguous(), prompt, strength, steps, guidance,
                         n_evals=2).images_u8.cpu()
     for i in range(3):
         one = eng.img2img(torch.from_numpy(imgs[i:i + 1]).to(device).contiguous(), prompt, strength, steps,
                           guidance, n_evals=2).images_u8.cpu()
-        assert (one[0].int() - batch[i].int()).abs().max() <= 2
+        assert torch.equal(one[0], batch[i])
