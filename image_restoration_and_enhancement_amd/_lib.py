@@ -104,10 +104,11 @@ EXPORTED = tuple(_SIGS)
 _lib = None
 
 
-def load(path: Path | str | None = None):
-    """Load libirx.so once; raises IrxError (never falls back) if it is missing."""
+def load(path: Path | str | None = None, force: bool = False):
+    """Load libirx.so once; raises IrxError (never falls back) if it is missing.  `force` re-resolves
+    `path` even when a library is already loaded (the loaded one stays in use if that fails)."""
     global _lib
-    if _lib is not None:
+    if _lib is not None and not force:
         return _lib
     p = Path(path) if path else LIB_PATH
     if not p.exists():

@@ -1,0 +1,169 @@
+"""Classical (non-diffusion) fallbacks of `RestorationPipeline` — numpy/scipy restatements of the OpenCV
+calls the reference makes when no diffusion model is available.
+
+cv2 is not installed on this image (neither here nor on the GPU box), so these are restatements of
+OpenCV's documented algorithms; where OpenCV uses a private approximation the result may differ by a
+few uint8 levels — parity unpinned (no oracle available), except where stated "exact":
+
+* `denoise_opencv`   — src/inference.py:500-522: fastNlMeansDenoisingColored(h, hColor, 7, 21) (non-local
+                       means in 8-bit CIELAB, L with h, a/b with hColor), then bilateralFilter(9, 75, 75)
+                       if strength > 0.6 and medianBlur(5) if strength > 0.8.
+* `sr_lanczos`       — src/inference.py:593-596: PIL LANCZOS resize (exact: same library call).
+* `colorize_lab`     — src/inference.py:683-703: L of RGB->LAB, a = L*0.1-10, b = L*0.1-5 as int8
+                       (negative values wrap through the uint8 cast exactly as the reference's
+                       `astype(np.uint8)` does), LAB->RGB.
+* `auto_mask`        — src/inference.py:805-840: RGB->GRAY (exact fixed-point), thresholds 30 / 225,
+                       5x5 close then open (exact), keep when >= 1 % of pixels.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+from PIL import Image
+from scipy.ndimage import grey_dilation, grey_erosion, median_filter
+
+# ---------------------------------------------------------------------------------------- colour
+_M_RGB2XYZ = np.array([[0.412453, 0.357580, 0.180423],
+                       [0.212671, 0.715160, 0.072169],
+                       [0.019334, 0.119193, 0.950227]])
+_WHITE = np.array([0.950456, 1.0, 1.088754])
+
+
+def rgb_to_gray_u8(rgb: np.ndarray) -> np.ndarray:
+    """cv2.cvtColor(RGB2GRAY) for uint8: (4899 R + 9617 G + 1868 B + 2^13) >> 14 (exact)."""
+    r, g, b = (rgb[..., i].astype(np.int64) for i in range(3))
+    return ((r * 4899 + g * 9617 + b * 1868 + (1 << 13)) >> 14).astype(np.uint8)
+
+
+def rgb_to_lab_u8(rgb: np.ndarray) -> np.ndarray:
+    """8-bit CIELAB as OpenCV stores it: L*255/100, a+128, b+128 (float arithmetic, rounded)."""
+    x = rgb.astype(np.float64) / 255.0
+    x = np.where(x > 0.04045, ((x + 0.055) / 1.055) ** 2.4, x / 12.92)
+    xyz = x @ _M_RGB2XYZ.T / _WHITE
+    f = np.where(xyz > 0.008856, np.cbrt(xyz), 7.787 * xyz + 16.0 / 116.0)
+    L = np.where(xyz[..., 1] > 0.008856, 116.0 * f[..., 1] - 16.0, 903.3 * xyz[..., 1])
+    a = 500.0 * (f[..., 0] - f[..., 1])
+    b = 200.0 * (f[..., 1] - f[..., 2])
+    out = np.stack([L * 255.0 / 100.0, a + 128.0, b + 128.0], -1)
+    return np.clip(np.rint(out), 0, 255).astype(np.uint8)
+
+
+def lab_u8_to_rgb(lab: np.ndarray) -> np.ndarray:
+    L = lab[..., 0].astype(np.float64) * 100.0 / 255.0
+    a = lab[..., 1].astype(np.float64) - 128.0
+    b = lab[..., 2].astype(np.float64) - 128.0
+    fy = (L + 16.0) / 116.0
+    fx, fz = fy + a / 500.0, fy - b / 200.0
+
+    def finv(t):
+        return np.where(t > 6.0 / 29.0, t ** 3, (t - 16.0 / 116.0) / 7.787)
+
+    y = np.where(L > 903.3 * 0.008856, fy ** 3, L / 903.3)
+    xyz = np.stack([finv(fx), y, finv(fz)], -1) * _WHITE
+    rgb = xyz @ np.linalg.inv(_M_RGB2XYZ).T
+    rgb = np.clip(rgb, 0.0, 1.0)
+    rgb = np.where(rgb > 0.0031308, 1.055 * rgb ** (1 / 2.4) - 0.055, 12.92 * rgb)
+    return np.clip(np.rint(rgb * 255.0), 0, 255).astype(np.uint8)
+
+
+# ---------------------------------------------------------------------------------------- filters
+def _box_sum(x: np.ndarray, r: int) -> np.ndarray:
+    """Sum over a (2r+1)^2 window of a reflect-101 padded [H, W] array."""
+    p = np.pad(x, r, mode="reflect")
+    c = np.cumsum(np.cumsum(p, 0), 1)
+    c = np.pad(c, ((1, 0), (1, 0)))
+    k = 2 * r + 1
+    return c[k:, k:] - c[:-k, k:] - c[k:, :-k] + c[:-k, :-k]
+
+
+def nl_means(img: np.ndarray, h: np.ndarray, template: int = 7, search: int = 21) -> np.ndarray:
+    """Non-local means over a [H, W, C] float image; per-channel filter strength h[C]:
+    w(p, q) = exp(-sum_c mean_patch (I_c(p) - I_c(q))^2 / h_c^2 / C)."""
+    H, W, C = img.shape
+    tr, sr = template // 2, search // 2
+    pad = np.pad(img, ((sr, sr), (sr, sr), (0, 0)), mode="reflect")
+    inv_h2 = 1.0 / np.maximum(np.asarray(h, np.float64) ** 2, 1e-12)
+    acc = np.zeros_like(img, dtype=np.float64)
+    wsum = np.zeros((H, W), np.float64)
+    area = float(template * template)
+    for dy in range(-sr, sr + 1):
+        for dx in range(-sr, sr + 1):
+            sh = pad[sr + dy:sr + dy + H, sr + dx:sr + dx + W]
+            d2 = ((img - sh) ** 2 * inv_h2).sum(-1) / C
+            dist = _box_sum(d2, tr) / area
+            w = np.exp(-np.maximum(dist, 0.0))
+            acc += w[..., None] * sh
+            wsum += w
+    return acc / wsum[..., None]
+
+
+def bilateral(img: np.ndarray, d: int = 9, sigma_color: float = 75.0, sigma_space: float = 75.0) -> np.ndarray:
+    """cv2.bilateralFilter for uint8 RGB: circular window of radius d//2, colour distance = sum of
+    per-channel absolute differences, reflect-101 borders."""
+    r = d // 2
+    x = img.astype(np.float64)
+    H, W, _ = x.shape
+    pad = np.pad(x, ((r, r), (r, r), (0, 0)), mode="reflect")
+    gc, gs = -0.5 / sigma_color ** 2, -0.5 / sigma_space ** 2
+    acc = np.zeros_like(x)
+    wsum = np.zeros((H, W))
+    for dy in range(-r, r + 1):
+        for dx in range(-r, r + 1):
+            rr = np.sqrt(dy * dy + dx * dx)
+            if rr > r:
+                continue
+            sh = pad[r + dy:r + dy + H, r + dx:r + dx + W]
+            cd = np.abs(sh - x).sum(-1)
+            w = np.exp(rr * rr * gs + cd * cd * gc)
+            acc += w[..., None] * sh
+            wsum += w
+    return np.clip(np.rint(acc / wsum[..., None]), 0, 255).astype(np.uint8)
+
+
+def median5(img: np.ndarray) -> np.ndarray:
+    """cv2.medianBlur(img, 5): per-channel 5x5 median with replicated borders."""
+    return median_filter(img, size=(5, 5, 1), mode="nearest")
+
+
+# ---------------------------------------------------------------------------------------- tasks
+def denoise_opencv(image: Image.Image, strength: float) -> Image.Image:
+    img = np.array(image.convert("RGB"))
+    hs = float(np.clip(strength, 0.1, 1.0))
+    h_value = hs * 10 if hs < 0.6 else 20          # luminance strength
+    h_color = hs * 10 if hs < 0.6 else 20          # chroma strength (same rule in the reference)
+    lab = rgb_to_lab_u8(img).astype(np.float64)
+    out = nl_means(lab, np.array([h_value, h_color, h_color]))
+    den = lab_u8_to_rgb(np.clip(np.rint(out), 0, 255).astype(np.uint8))
+    if strength > 0.6:
+        den = bilateral(den, 9, 75, 75)
+    if strength > 0.8:
+        den = median5(den)
+    return Image.fromarray(den)
+
+
+def sr_lanczos(image: Image.Image, scale: int) -> Image.Image:
+    w, h = image.size
+    return image.resize((w * scale, h * scale), Image.LANCZOS)
+
+
+def colorize_lab(image: Image.Image) -> Image.Image:
+    img = np.array(image.convert("RGB"))
+    L = rgb_to_lab_u8(img)[..., 0]
+    a = np.clip(L * 0.1 - 10, -127, 127).astype(np.int8)
+    b = np.clip(L * 0.1 - 5, -127, 127).astype(np.int8)
+    lab = np.stack([L, a, b], axis=2)             # int8 promotes; the uint8 cast below wraps negatives
+    return Image.fromarray(lab_u8_to_rgb(lab.astype(np.uint8)))
+
+
+def auto_mask(image: Image.Image) -> Optional[Image.Image]:
+    gray = rgb_to_gray_u8(np.array(image.convert("RGB")))
+    m = np.where((gray <= 30) | (gray > 225), 255, 0).astype(np.uint8)
+    fp = np.ones((5, 5), bool)
+    m = grey_erosion(grey_dilation(m, footprint=fp, mode="constant", cval=0), footprint=fp, mode="constant",
+                     cval=255)                                               # MORPH_CLOSE
+    m = grey_dilation(grey_erosion(m, footprint=fp, mode="constant", cval=255), footprint=fp, mode="constant",
+                      cval=0)                                                # MORPH_OPEN
+    if np.sum(m > 0) / m.size < 0.01:
+        return None
+    return Image.fromarray(m).convert("L")

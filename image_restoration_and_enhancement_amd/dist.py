@@ -50,6 +50,24 @@ def broadcast_blobs(blobs: Dict[str, torch.Tensor], src: int = 0) -> Dict[str, t
     return blobs
 
 
+def gather_shards(shard: torch.Tensor, n_total: int) -> torch.Tensor:
+    """Reassemble the per-rank contiguous shards (dim 0, as produced by shard_range) into the full batch
+    on every rank — one all_gather of the outputs at the end of a job, never inside the step loop."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return shard
+    world = dist.get_world_size()
+    per = (n_total + world - 1) // world
+    buf = torch.zeros((per,) + tuple(shard.shape[1:]), dtype=shard.dtype, device=shard.device)
+    buf[:shard.shape[0]] = shard
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    out = []
+    for r in range(world):
+        s, e = shard_range(n_total, r, world)
+        out.append(parts[r][:e - s])
+    return torch.cat(out, 0)
+
+
 def max_over_ranks(x: float, device=None) -> float:
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return float(x)

@@ -53,3 +53,43 @@ def stroke_mask(h: int, w: int, seed: int = 0) -> np.ndarray:
 
 def pil(a: np.ndarray) -> Image.Image:
     return Image.fromarray(a)
+
+
+def save_model_dir(root, task: str, seed: int = 0, dtype=torch.float16):
+    """Write a diffusers-layout `best/` directory (configs + safetensors) holding the seeded weights, the
+    way `pipeline.save_pretrained()` lays it out (outputs/models/*/best/), minus the tokenizer files."""
+    import json
+    from pathlib import Path
+    from safetensors.torch import save_file
+
+    pc, sd = state_dicts(task, seed)
+    root = Path(root)
+    u, v, c = pc.unet, pc.vae, pc.clip
+    cfgs = {
+        "unet/config.json": {"_class_name": "UNet2DConditionModel", "in_channels": u.in_channels,
+                             "out_channels": u.out_channels, "block_out_channels": u.block_out_channels,
+                             "layers_per_block": u.layers_per_block, "attention_head_dim": u.attention_heads,
+                             "cross_attention_dim": u.cross_attention_dim, "norm_num_groups": u.norm_num_groups,
+                             "norm_eps": u.norm_eps, "sample_size": u.sample_size,
+                             "down_block_types": ["CrossAttnDownBlock2D"] * 3 + ["DownBlock2D"],
+                             "up_block_types": ["UpBlock2D"] + ["CrossAttnUpBlock2D"] * 3,
+                             "use_linear_projection": False},
+        "vae/config.json": {"_class_name": "AutoencoderKL", "block_out_channels": v.block_out_channels,
+                            "latent_channels": v.latent_channels, "scaling_factor": v.scaling_factor},
+        "text_encoder/config.json": {"architectures": ["CLIPTextModel"], "hidden_act": c.hidden_act,
+                                     "hidden_size": c.hidden_size, "num_hidden_layers": c.num_hidden_layers},
+        "scheduler/scheduler_config.json": {"_class_name": "DDIMScheduler" if task == "inpaint" else "PNDMScheduler",
+                                            "beta_schedule": "scaled_linear", "beta_start": 0.00085,
+                                            "beta_end": 0.012, "num_train_timesteps": 1000, "steps_offset": 1,
+                                            "set_alpha_to_one": False, "skip_prk_steps": True,
+                                            "clip_sample": False},
+    }
+    for rel, d in cfgs.items():
+        f = root / rel
+        f.parent.mkdir(parents=True, exist_ok=True)
+        f.write_text(json.dumps(d))
+    for comp, fname, key in (("unet", "diffusion_pytorch_model.safetensors", "unet"),
+                             ("vae", "diffusion_pytorch_model.safetensors", "vae"),
+                             ("text_encoder", "model.safetensors", "clip")):
+        save_file({k: t.to(dtype).contiguous() for k, t in sd[key].items()}, str(root / comp / fname))
+    return root

@@ -1,0 +1,93 @@
+"""GPU tests of the drop-in `RestorationPipeline` (src/inference.py surface) on the native engine:
+end-to-end against the CPU oracle, loading a saved diffusers-layout model directory, batched == single,
+and the reference's `process()` quirk (denoise reached through process runs the classical fallback)."""
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from image_restoration_and_enhancement_amd import classical as CL
+from image_restoration_and_enhancement_amd import inference as INF
+from image_restoration_and_enhancement_amd.pipelines import SDEngine
+from oracle import pipeline_ref as PR
+from tests import models_common as MC
+
+pytestmark = pytest.mark.gpu
+
+RANDOM = {"fine_tuned_dir": "unused", "pretrained_id": "unused", "weights": "random"}
+
+
+def cfg(dtype="fp32", **tasks):
+    c = {"engine": {"dtype": dtype}}
+    c.update({t: dict(RANDOM) for t in tasks.get("random", ())})
+    return c
+
+
+def test_denoise_matches_oracle_fp32(device):
+    """Full reference call (strength 0.5, 20 PNDM steps -> 11 evals, guidance 5, seed 42) at 64x64."""
+    p = INF.RestorationPipeline(device="cuda", config=cfg("fp32", random=["denoise"]))
+    img = MC.pil(MC.smooth_image(64, 64, seed=11))
+    out = p.denoise(img)
+    assert isinstance(p.models["denoise"], INF.NativeSDModel)
+    prompt, strength, steps, guidance = PR.TASKS["denoise"]
+    ref = PR.img2img_ref(MC.oracle_models("denoise"), img, MC.prompt_ids(prompt), MC.prompt_ids(""), strength,
+                         steps, guidance, 42, "pndm")
+    d = np.abs(np.asarray(out).astype(int) - np.asarray(ref.image).astype(int))
+    assert out.size == (64, 64)
+    assert d.max() <= 1 and (d > 0).mean() < 0.01
+
+
+def test_sr_and_colorize_share_engine(device):
+    p = INF.RestorationPipeline(device="cuda", config=cfg("bf16", random=["sr", "colorize"]))
+    a = p.super_resolve(MC.pil(MC.smooth_image(40, 48, seed=1)))
+    gray = np.repeat(MC.smooth_image(48, 40, seed=2)[..., :1], 3, axis=2)
+    b = p.colorize(Image.fromarray(gray))
+    assert a.size == (48, 40) and b.size == (40, 48)
+    assert p.models["sr"].engine is p.models["colorize"].engine
+
+
+def test_model_dir_loading(device, tmp_path):
+    """A saved best/ directory (fp16 safetensors + diffusers configs) drives the engine: the result equals an
+    engine built from the same (fp16-rounded) weights in memory."""
+    root = MC.save_model_dir(tmp_path / "denoising" / "best", "denoise", dtype=torch.float16)
+    p = INF.RestorationPipeline(device="cuda", config={"engine": {"dtype": "bf16"},
+                                                       "denoise": {"fine_tuned_dir": str(root),
+                                                                   "pretrained_id": "unused"}})
+    img = MC.pil(MC.smooth_image(32, 48, seed=3))
+    out = p.denoise(img, strength=0.3)
+    assert p.models["denoise"].source == str(root)
+    pc, sd = MC.state_dicts("denoise")
+    sd16 = {k: {n: t.half().float() for n, t in v.items()} for k, v in sd.items()}
+    eng = SDEngine(pc, "bf16", device, state_dicts=sd16)
+    u8 = torch.from_numpy(np.asarray(img)).to(device)[None].contiguous()
+    prompt = p.prompts["denoise"]
+    ref = eng.img2img(u8, prompt, 0.3, 20, 5.0, seed=42).images_u8[0].cpu().numpy()
+    assert np.array_equal(np.asarray(out), ref)
+
+
+def test_restore_batch_equals_single_calls(device):
+    p = INF.RestorationPipeline(device="cuda", config=cfg("fp32", random=["denoise"]))
+    imgs = [MC.pil(MC.smooth_image(64, 64, seed=s)) for s in (4, 5, 6)] + [MC.pil(MC.smooth_image(40, 56, seed=7))]
+    batch = p.restore_batch("denoise", imgs)
+    for im, b in zip(imgs, batch):
+        assert np.array_equal(np.asarray(p.denoise(im)), np.asarray(b))
+
+
+def test_inpaint_runs_at_512(device):
+    p = INF.RestorationPipeline(device="cuda", config=cfg("bf16", random=["inpaint"]))
+    img = MC.pil(MC.smooth_image(96, 80, seed=8))
+    mask = MC.pil(MC.stroke_mask(96, 80, seed=8))
+    out = p.inpaint(img, mask=mask)
+    assert out.size == (512, 512)
+    out2 = p.restore_batch("inpaint", [img, img], masks=[mask, mask])
+    assert all(np.array_equal(np.asarray(out), np.asarray(o)) for o in out2)
+
+
+def test_process_denoise_uses_classical_fallback(device):
+    """The reference's process() passes prompt=None to denoise; the diffusion call rejects it and the
+    classical fallback runs (src/inference.py:489-498, :859-864) — reproduced."""
+    p = INF.RestorationPipeline(device="cuda", config=cfg("bf16", random=["denoise"]))
+    img = MC.pil(MC.smooth_image(24, 24, seed=9))
+    res = p.process(img, ["denoise"])
+    assert isinstance(p.models["denoise"], INF.NativeSDModel)
+    assert np.array_equal(np.asarray(res["denoised"]), np.asarray(CL.denoise_opencv(img, 0.5)))
