@@ -418,8 +418,9 @@ class RestorationPipeline:
                       prompt: Optional[str] = None, strength: Optional[float] = None,
                       max_batch: int = 8) -> List[Image.Image]:
         """Batched form of the single-image entry points (new; the reference loops one image per call).
-        Images of equal processed size run as one engine batch of up to `max_batch`; each image gets
-        exactly the result the single-image call returns (per-call reseeded noise).  Falls back to the
+        Images of equal processed size run as one engine batch of up to `max_batch`; each image gets the
+        result the single-image call returns (per-call reseeded noise) — bit-exactly on the fp32 engine; on
+        bf16 a different batch size may select another GEMM tiling / split-K, i.e. different rounding.  Falls back to the
         single-image entry point per image whenever that one would not take the diffusion path."""
         task = "sr" if task == "super_resolution" else task
         loader = {"denoise": self.load_denoise_model, "sr": self.load_sr_model,

@@ -59,7 +59,7 @@ def test_model_dir_loading(device, tmp_path):
     pc, sd = MC.state_dicts("denoise")
     sd16 = {k: {n: t.half().float() for n, t in v.items()} for k, v in sd.items()}
     eng = SDEngine(pc, "bf16", device, state_dicts=sd16)
-    u8 = torch.from_numpy(np.asarray(img)).to(device)[None].contiguous()
+    u8 = torch.from_numpy(np.array(img)).to(device)[None].contiguous()
     prompt = p.prompts["denoise"]
     ref = eng.img2img(u8, prompt, 0.3, 20, 5.0, seed=42).images_u8[0].cpu().numpy()
     assert np.array_equal(np.asarray(out), ref)
@@ -74,7 +74,8 @@ def test_restore_batch_equals_single_calls(device):
 
 
 def test_inpaint_runs_at_512(device):
-    p = INF.RestorationPipeline(device="cuda", config=cfg("bf16", random=["inpaint"]))
+    """fp32 engine: batched == single bit-exactly (bf16 may pick another GEMM split for another batch)."""
+    p = INF.RestorationPipeline(device="cuda", config=cfg("fp32", random=["inpaint"]))
     img = MC.pil(MC.smooth_image(96, 80, seed=8))
     mask = MC.pil(MC.stroke_mask(96, 80, seed=8))
     out = p.inpaint(img, mask=mask)
