@@ -77,6 +77,19 @@ def build_engine(cfg, dtype, device, rank):
     return eng, sds
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (scripts/pmc_traffic.py;
+    FETCH_SIZE x2 + WRITE_SIZE per the gfx950 note), or None when no pass for this kernel is committed."""
+    for f in sorted(Path(__file__).resolve().parent.glob("profiles/*pmc_traffic*.json"), reverse=True):
+        try:
+            d = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") and d["kernel"] in kernel:
+            return round(d["bytes_per_launch"])
+    return None
+
+
 def cpu_baseline(cfg, sds, res: int, steps: int, strength: float, threads: int) -> dict:
     """fp32 CPU restatement: 1 image; VAE encode + 1 CFG UNet eval (batch 2) + VAE decode, extrapolated
     to the full per-image schedule (n_evals UNet evals)."""
@@ -177,7 +190,7 @@ def main():
         peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
         ach = fl / (ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(ach / peak, 4), "traffic": None, "kernel": name,
+                    "frac": round(ach / peak, 4), "traffic": pmc_traffic(name), "kernel": name,
                     "launches": cnt, "avg_launch_us": round(ms * 1e3 / cnt, 2),
                     "flops_per_launch": fl / cnt,
                     "all_mfma_kernels_tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 2)}
