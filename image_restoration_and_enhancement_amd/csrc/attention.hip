@@ -468,9 +468,8 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
 
 void launch_bf16(const AttnArgs& a, hipStream_t s) {
   dim3 grid((a.Lq + kQB - 1) / kQB, a.H, a.B), block(256);
-  const int dq = (a.d + 31) / 32 * 32;
-  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn2_kernel<") + std::to_string(dq) + ">"
-                         : std::string(),
+  const char* inst = a.d == 40 ? "64, 48, 128" : a.d == 64 ? "64, 64, 128" : a.d == 80 ? "96, 80, 64" : "160, 160, 32";
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn2_kernel<") + inst + ">" : std::string(),
                4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
   switch (a.d) {
     case 40: attn2_kernel<64, 48, 128><<<grid, block, 0, s>>>(a); break;

@@ -337,14 +337,14 @@ template <int BM, int BN, int WM, int WN>
 void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, a.batch * sp.splits), block(512);
+  const bool rs = a.conv && (a.g.Hv != a.g.Hin || a.g.Wv != a.g.Win);
   std::string nm;
-  if (prof_on())
+  if (prof_on())   // same spelling as the demangled name rocprofv3 reports
     nm = "irx::(anonymous namespace)::gemm2_kernel<" + std::to_string(BM) + ", " + std::to_string(BN) + ", " +
          std::to_string(WM) + ", " + std::to_string(WN) + ", " + (a.conv ? "true" : "false") + ", " +
-         (a.out_f32 ? "true" : "false") + ">";
+         (a.out_f32 ? "true" : "false") + ", " + (rs ? "true" : "false") + ">";
   {
     ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
-    const bool rs = a.conv && (a.g.Hv != a.g.Hin || a.g.Wv != a.g.Win);
     if (a.conv) {   // (fp32-output convs never take this path: see eligible())
       if (rs) gemm2_kernel<BM, BN, WM, WN, true, false, true><<<grid, block, 0, s>>>(a, sp);
       else gemm2_kernel<BM, BN, WM, WN, true, false, false><<<grid, block, 0, s>>>(a, sp);

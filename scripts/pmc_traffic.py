@@ -12,11 +12,18 @@ from __future__ import annotations
 import argparse
 import csv
 import json
+import sqlite3
 from pathlib import Path
 
 
 def per_launch(d: Path, counter: str, kernel: str):
     vals = {}
+    for f in Path(d).rglob("*results.db"):            # rocprofv3's default rocpd (sqlite) output
+        con = sqlite3.connect(str(f))
+        for disp, name, v in con.execute("select dispatch_id, kernel_name, value from counters_collection "
+                                         "where counter_name = ?", (counter,)):
+            if kernel in name:
+                vals[(f, disp)] = vals.get((f, disp), 0.0) + float(v)
     for f in Path(d).rglob("*counter_collection.csv"):
         with open(f) as fh:
             for row in csv.DictReader(fh):
