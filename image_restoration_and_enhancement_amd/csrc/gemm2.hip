@@ -35,14 +35,43 @@ struct Split {
   float* ws = nullptr; // fp32 partials [batch*splits][M][N]
 };
 
-template <int BM, int BN, int WM, int WN, bool CONV, bool OUTF32, bool RESIZE>
+// Wait until at most n of this wave's vector-memory operations (here: LDS-DMA pieces) are outstanding.
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+#define IRX_VM(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    IRX_VM(0) IRX_VM(1) IRX_VM(2) IRX_VM(3) IRX_VM(4) IRX_VM(5) IRX_VM(6) IRX_VM(7) IRX_VM(8) IRX_VM(9)
+    IRX_VM(10) IRX_VM(11) IRX_VM(12) IRX_VM(13) IRX_VM(14) IRX_VM(15) IRX_VM(16) IRX_VM(18) IRX_VM(20)
+    IRX_VM(21) IRX_VM(24) IRX_VM(28) IRX_VM(30) IRX_VM(32) IRX_VM(35) IRX_VM(36) IRX_VM(40) IRX_VM(42)
+    IRX_VM(45) IRX_VM(48) IRX_VM(49) IRX_VM(54) IRX_VM(56) IRX_VM(60)
+#undef IRX_VM
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// 16-byte LDS-DMA piece issued from inline asm: the compiler does not see the LDS write, so it cannot
+// insert its own conservative vmcnt(0) in front of every ds_read (it cannot prove the ring stages
+// disjoint); the ring's counted waits + s_barrier below provide the ordering instead.
+__device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds_addr)
+               : "memory", "m0");
+}
+
+// BK: K depth of one LDS stage (64: 8 chunks of 16 B per row, 32: 4); S: stages in the ring.
+// S == 2 is the classic double buffer (drain + barrier per step); S > 2 keeps S-2 stages of LDS-DMA in
+// flight across each (raw) barrier, waiting with a counted vmcnt for exactly the stage about to be read.
+template <int BM, int BN, int WM, int WN, int BK, int S, bool CONV, bool OUTF32, bool RESIZE>
 __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int ROWS = BM + BN;
-  constexpr int NINST = ROWS / 8;            // 1 KiB LDS-DMA wave instructions per stage (8 rows each)
-  constexpr int IPW = NINST / 8;             // per wave
-  static_assert(WM * WN == 8 && NINST % 8 == 0 && BM % 64 == 0, "tile shape");
-  __shared__ __attribute__((aligned(16))) uint4 smem[2 * ROWS * 8];
+  constexpr int CPR = BK / 8;                // 16-byte chunks per row per stage
+  constexpr int RPI = 64 / CPR;              // rows per 1 KiB LDS-DMA wave instruction
+  constexpr int NINST = ROWS / RPI;          // wave instructions per stage
+  constexpr int IPW = (NINST + 7) / 8;       // per wave (the surplus ones are dummies into a scratch KiB)
+  constexpr int STAGE = ROWS * CPR;          // uint4 per stage
+  constexpr int KSUB = BK / 32;              // 32-deep MFMA sub-steps per stage
+  static_assert(WM * WN == 8 && ROWS % RPI == 0 && BM % 16 == 0 && (BK == 32 || BK == 64), "tile shape");
+  constexpr int SMEM = (S * STAGE > BM * BN / 8 ? S * STAGE : BM * BN / 8) + (NINST % 8 ? 64 : 0);
+  __shared__ __attribute__((aligned(16))) uint4 smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -52,28 +81,32 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
   const int tile_n = bid % tiles_n, tile_m = bid / tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int z = blockIdx.y / sp.splits, ks = blockIdx.y % sp.splits;
-  const int nk_all = a.K / 64;
+  const int nk_all = a.K / BK;
   const int kt0 = ks * sp.per;
   const int kt1 = min(nk_all, kt0 + sp.per);
   const uint16_t* __restrict__ Bp = (const uint16_t*)a.B + (long)z * a.sB;
   const uint16_t* __restrict__ Ap = CONV ? nullptr : (const uint16_t*)a.A + (long)z * a.sA;
   const uint16_t* zp = (const uint16_t*)g_zero_page;
 
-  // ---- per-lane DMA assignment: instruction j of this wave covers rows 8*(wave*IPW + j) .. +7;
+  // ---- per-lane DMA assignment: instruction q = wave*IPW + j covers rows RPI*q .. +RPI-1;
   //      lane -> row + 16-byte slot; it fetches the logical chunk slot ^ swz(row)
   // Each lane keeps a row base pointer (nullptr = zero page) and adds a block-uniform K offset per step;
   // conv rows re-derive their base only when the K walk enters a new tap or the concat's second source.
-  const int lrow = lane >> 3, lslot = lane & 7;
-  bool isA[IPW];
-  int lk[IPW];                       // this lane's element offset in the 64-deep K step (logical chunk * 8)
+  auto swz = [](int r) { return CPR == 8 ? ((r >> 1) & 7) : ((r >> 2) & 3); };
+  const int lrow = lane / CPR, lslot = lane % CPR;
+  bool isA[IPW], live[IPW];
+  int lk[IPW];                       // this lane's element offset in the K step (logical chunk * 8)
   int rn[IPW], riy[IPW], rix[IPW];   // conv A rows: image index (-1 invalid), receptive-field origin
   const uint16_t* rb[IPW];           // current row base (nullptr if out of range / padded tap)
 #pragma unroll
   for (int j = 0; j < IPW; ++j) {
-    const int r = 8 * (wave * IPW + j) + lrow;
-    isA[j] = r < BM;
-    lk[j] = (lslot ^ ((r >> 1) & 7)) * 8;
+    const int q = wave * IPW + j;
+    const int r = RPI * q + lrow;
+    live[j] = q < NINST;
+    isA[j] = live[j] && r < BM;
+    lk[j] = (lslot ^ swz(r)) * 8;
     rn[j] = -1; riy[j] = 0; rix[j] = 0; rb[j] = nullptr;
+    if (!live[j]) continue;
     if (r < BM) {
       const int m = m0 + r;
       if (m < a.M) {
@@ -116,7 +149,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
     }
   };
   if constexpr (CONV) {
-    const int k = kt0 * 64;
+    const int k = kt0 * BK;
     const int tap = k / Cin;
     kc = k - tap * Cin;
     ky = tap / a.g.KW;
@@ -125,16 +158,21 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
   }
 
   auto issue = [&](int kt, int stage) {
-    uint4* sbase = smem + stage * ROWS * 8;
-    const int koffA = CONV ? (kc >= a.g.C0 ? kc - a.g.C0 : kc) : kt * 64;
-    const int koffB = kt * 64;
+    uint4* sbase = smem + stage * STAGE;
+    const int koffA = CONV ? (kc >= a.g.C0 ? kc - a.g.C0 : kc) : kt * BK;
+    const int koffB = kt * BK;
 #pragma unroll
     for (int j = 0; j < IPW; ++j) {
       const uint16_t* src = rb[j] ? rb[j] + ((isA[j] ? koffA : koffB) + lk[j]) : zp;
-      __builtin_amdgcn_global_load_lds(src, (lds_void*)(sbase + (wave * IPW + j) * 64), 16, 0, 0);
+      uint4* dst = live[j] ? sbase + (wave * IPW + j) * 64 : smem + SMEM - 64;
+      if constexpr (S == 2) {
+        __builtin_amdgcn_global_load_lds(src, (lds_void*)dst, 16, 0, 0);
+      } else {
+        glds16_asm(src, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
+      }
     }
     if constexpr (CONV) {
-      kc += 64;
+      kc += BK;
       if (kc == Cin) {
         kc = 0;
         if (++kx == a.g.KW) { kx = 0; ++ky; }
@@ -152,38 +190,71 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int frow = lane & 15, fgrp = lane >> 4;
-  if (kt0 < kt1) issue(kt0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int st = (kt - kt0) & 1;
-    if (kt + 1 < kt1) issue(kt + 1, st ^ 1);
-    const uint4* As = smem + st * ROWS * 8;
-    const uint4* Bs = As + BM * 8;
+  auto compute = [&](int st) {
+    const uint4* As = smem + st * STAGE;
+    const uint4* Bs = As + BM * CPR;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < KSUB; ++s) {
       uint4 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * TM * 16 + i * 16 + frow;
-        af[i] = As[r * 8 + ((s * 4 + fgrp) ^ ((r >> 1) & 7))];
+        af[i] = As[r * CPR + ((s * 4 + fgrp) ^ swz(r))];
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = wn * TN * 16 + j * 16 + frow;
-        bfr[j] = Bs[r * 8 + ((s * 4 + fgrp) ^ (((r + BM) >> 1) & 7))];
+        bfr[j] = Bs[r * CPR + ((s * 4 + fgrp) ^ swz(r + BM))];
       }
+      if constexpr (S > 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
                                                               __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+      if constexpr (S > 2) __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  if constexpr (S == 2) {
+    if (kt0 < kt1) issue(kt0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int st = (kt - kt0) & 1;
+      if (kt + 1 < kt1) issue(kt + 1, st ^ 1);
+      if (!(a.dbg & 2)) compute(st);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // prologue: stages 0 .. S-2 in flight
+#pragma unroll
+    for (int p = 0; p < S - 1; ++p)
+      if (kt0 + p < kt1) issue(kt0 + p, p);
+    int st = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      // this wave's pieces of step kt have landed once at most min(S-2, kt1-1-kt) younger stages remain
+      wait_vm(IPW * min(S - 2, kt1 - 1 - kt));
+      asm volatile("s_barrier" ::: "memory");   // everyone's pieces landed; everyone finished reading kt-1
+      if (kt + S - 1 < kt1) issue(kt + S - 1, st == 0 ? S - 1 : st - 1);
+      if (!(a.dbg & 2)) compute(st);
+      st = st + 1 == S ? 0 : st + 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
+  if (a.dbg & 1) {   // diagnostics: keep the accumulators live, skip the output
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 12345.678f) ((float*)a.C)[0] = t;
+    return;
+  }
   // ---- split-K: raw fp32 partial tile, epilogue applied by splitk_reduce_kernel
   if (sp.splits > 1) {
     float* P = sp.ws + (long)blockIdx.y * a.M * a.N;
@@ -209,7 +280,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
       // (16-byte chunks XOR-swizzled by row to spread banks); pass 2 streams whole 16-byte row chunks out,
       // adding the residual and applying out_scale, or (GEGLU) combining each 64-wide value block with its
       // gate block h * gelu(g) and writing half-width rows.
-      static_assert(BM * BN * 2 <= 2 * ROWS * 8 * 16, "epilogue tile must fit the staging LDS");
+      static_assert(BM * BN * 2 <= SMEM * 16, "epilogue tile must fit the staging LDS");
       uint16_t* tileS = (uint16_t*)smem;
       uint16_t* Cp = (uint16_t*)a.C + (long)z * a.sC;
       const int act1 = a.geglu ? (int)ACT_NONE : a.act;
@@ -333,7 +404,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int BK, int S>
 void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, a.batch * sp.splits), block(512);
@@ -341,16 +412,17 @@ void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
   std::string nm;
   if (prof_on())   // same spelling as the demangled name rocprofv3 reports
     nm = "irx::(anonymous namespace)::gemm2_kernel<" + std::to_string(BM) + ", " + std::to_string(BN) + ", " +
-         std::to_string(WM) + ", " + std::to_string(WN) + ", " + (a.conv ? "true" : "false") + ", " +
-         (a.out_f32 ? "true" : "false") + ", " + (rs ? "true" : "false") + ">";
+         std::to_string(WM) + ", " + std::to_string(WN) + ", " + std::to_string(BK) + ", " + std::to_string(S) +
+         ", " + (a.conv ? "true" : "false") + ", " + (a.out_f32 ? "true" : "false") + ", " +
+         (rs ? "true" : "false") + ">";
   {
     ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
     if (a.conv) {   // (fp32-output convs never take this path: see eligible())
-      if (rs) gemm2_kernel<BM, BN, WM, WN, true, false, true><<<grid, block, 0, s>>>(a, sp);
-      else gemm2_kernel<BM, BN, WM, WN, true, false, false><<<grid, block, 0, s>>>(a, sp);
+      if (rs) gemm2_kernel<BM, BN, WM, WN, BK, S, true, false, true><<<grid, block, 0, s>>>(a, sp);
+      else gemm2_kernel<BM, BN, WM, WN, BK, S, true, false, false><<<grid, block, 0, s>>>(a, sp);
     } else {
-      if (a.out_f32) gemm2_kernel<BM, BN, WM, WN, false, true, false><<<grid, block, 0, s>>>(a, sp);
-      else gemm2_kernel<BM, BN, WM, WN, false, false, false><<<grid, block, 0, s>>>(a, sp);
+      if (a.out_f32) gemm2_kernel<BM, BN, WM, WN, BK, S, false, true, false><<<grid, block, 0, s>>>(a, sp);
+      else gemm2_kernel<BM, BN, WM, WN, BK, S, false, false, false><<<grid, block, 0, s>>>(a, sp);
     }
     IRX_LAUNCH_CHECK();
   }
@@ -370,9 +442,11 @@ struct Choice {
   int BM = 0, BN = 0, splits = 1, per = 0;
 };
 
+int step_k() { return g_gemm_deep ? 32 : 64; }   // K depth of one pipeline stage
+
 Choice choose(const GemmArgs& a) {
   Choice best;
-  const int nk = a.K / 64;
+  const int nk = a.K / step_k();
   double best_score = -1.0;
   const int cands[5][2] = {{256, 256}, {128, 320}, {256, 128}, {128, 256}, {128, 128}};
   for (auto& c : cands) {
@@ -384,7 +458,7 @@ Choice choose(const GemmArgs& a) {
     for (int splits = 1; splits <= 8; splits *= 2) {
       if (splits > 1 && ((a.out_f32 && a.batch > 1) || a.geglu)) break;
       const int per = (nk + splits - 1) / splits;
-      if (per < 8 && splits > 1) break;                 // keep >= 8 K steps per split
+      if (per * step_k() < 512 && splits > 1) break;    // keep >= 512 of K per split
       if ((long)(splits - 1) * per >= nk) break;        // no empty split
       const long blocks = tiles * splits;
       const double util = (double)blocks / ((double)((blocks + kCUs - 1) / kCUs) * kCUs);
@@ -416,10 +490,11 @@ float* internal_ws(size_t bytes) {
 }
 
 bool eligible(const GemmArgs& a) {
-  if (a.dtype != BF16 || a.K % 64 != 0 || a.ldb % 8 != 0) return false;
+  const int bk = step_k();
+  if (a.dtype != BF16 || a.K % bk != 0 || a.ldb % 8 != 0) return false;
   if ((long)a.M * a.batch < 512) return false;     // tiny outputs: the 64x64 4-wave tiles waste less
   if (a.geglu && (a.out_f32 || a.residual || a.batch != 1 || a.N % 128 != 0)) return false;
-  if (a.conv) return !a.out_f32 && a.g.C0 % 64 == 0 && a.g.C1 % 64 == 0;
+  if (a.conv) return !a.out_f32 && a.g.C0 % bk == 0 && a.g.C1 % bk == 0;
   return a.lda % 8 == 0 && (a.batch == 1 || a.sA % 8 == 0);
 }
 
@@ -430,6 +505,9 @@ bool vec_ok(const GemmArgs& a) {
 }
 
 }  // namespace
+
+bool g_gemm_deep = false;  // irx_set_option("gemm_deep", 1): S-stage BK=32 ring (measured slower; A/B tests)
+int g_gemm_dbg = 0;   // irx_set_option("gemm_deep", 0): 2-stage BK=64 loop (A/B tests)
 
 bool gemm_geglu_fusable(const GemmArgs& a) {
   if (!g_large_tiles || !a.geglu || !eligible(a) || !vec_ok(a)) return false;
@@ -450,6 +528,7 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   if (c.BM == 0) return false;
   GemmArgs b = a;
   b.vec_epilogue = vec_ok(a);
+  b.dbg = g_gemm_dbg;
   if (a.geglu && !b.vec_epilogue) return false;
   Split sp;
   sp.splits = c.splits;
@@ -460,15 +539,26 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     const size_t need = (size_t)c.splits * a.batch * a.M * a.N * sizeof(float);
     sp.ws = (a.splitk_ws && a.splitk_ws_bytes >= need) ? (float*)a.splitk_ws : internal_ws(need);
   } else {
-    sp.per = a.K / 64;
+    sp.per = a.K / step_k();
   }
-  switch (c.BM * 1000 + c.BN) {
-    case 256256: launch2<256, 256, 2, 4>(b, sp, s); break;
-    case 128320: launch2<128, 320, 2, 4>(b, sp, s); break;
-    case 256128: launch2<256, 128, 4, 2>(b, sp, s); break;
-    case 128256: launch2<128, 256, 2, 4>(b, sp, s); break;
-    case 128128: launch2<128, 128, 2, 4>(b, sp, s); break;
-    default: return false;
+  if (g_gemm_deep) {
+    switch (c.BM * 1000 + c.BN) {
+      case 256256: launch2<256, 256, 2, 4, 32, 4>(b, sp, s); break;
+      case 128320: launch2<128, 320, 2, 4, 32, 5>(b, sp, s); break;
+      case 256128: launch2<256, 128, 4, 2, 32, 5>(b, sp, s); break;
+      case 128256: launch2<128, 256, 2, 4, 32, 5>(b, sp, s); break;
+      case 128128: launch2<128, 128, 2, 4, 32, 6>(b, sp, s); break;
+      default: return false;
+    }
+  } else {
+    switch (c.BM * 1000 + c.BN) {
+      case 256256: launch2<256, 256, 2, 4, 64, 2>(b, sp, s); break;
+      case 128320: launch2<128, 320, 2, 4, 64, 2>(b, sp, s); break;
+      case 256128: launch2<256, 128, 4, 2, 64, 2>(b, sp, s); break;
+      case 128256: launch2<128, 256, 2, 4, 64, 2>(b, sp, s); break;
+      case 128128: launch2<128, 128, 2, 4, 64, 2>(b, sp, s); break;
+      default: return false;
+    }
   }
   return true;
 }

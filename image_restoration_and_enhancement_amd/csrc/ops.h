@@ -40,12 +40,15 @@ struct GemmArgs {
   // columns h * gelu(g).  Only the large-tile path fuses it (gemm_geglu_fusable); else see geglu().
   int geglu = 0;
   void* splitk_ws = nullptr; size_t splitk_ws_bytes = 0;   // caller workspace for split-K partials
+  int dbg = 0;            // large-tile diagnostics (irx_set_option("gemm_dbg")): 1 skip epilogue, 2 skip MFMAs
 };
 void gemm(const GemmArgs& a, hipStream_t s);
 bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path; false if not eligible
 size_t gemm_workspace_bytes(const GemmArgs& a);           // split-K partial buffer the call will use
 bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can apply the GEGLU epilogue
 extern bool g_large_tiles;
+extern bool g_gemm_deep;
+extern int g_gemm_dbg;     // timing diagnostics only: results are wrong when set   // large-tile path: S-stage BK=32 LDS-DMA ring (else 2-stage BK=64)
 
 // ------------------------------------------------------------ normalisation
 // GroupNorm over NHWC (optionally a channel concat of two sources). Writes the normalised (and

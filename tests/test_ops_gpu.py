@@ -209,12 +209,14 @@ def test_geglu(device, dt):
 
 
 # ------------------------------------------------------------------ large-tile (8-wave LDS-DMA) path
-@pytest.fixture(params=[1, 0], ids=["large_tiles", "4wave"])
+@pytest.fixture(params=[(1, 1), (1, 0), (0, 1)], ids=["deep_ring", "two_stage", "4wave"])
 def tiles(request):
     from image_restoration_and_enhancement_amd import _lib as L
-    L.call("irx_set_option", b"large_tiles", request.param)
+    L.call("irx_set_option", b"large_tiles", request.param[0])
+    L.call("irx_set_option", b"gemm_deep", request.param[1])
     yield request.param
     L.call("irx_set_option", b"large_tiles", 1)
+    L.call("irx_set_option", b"gemm_deep", 0)
 
 
 @pytest.mark.parametrize("case", [
@@ -224,6 +226,8 @@ def tiles(request):
     (4, 16, 16, 1280, 0, 1280, 3, 1, 1, (32, 32)),  # Upsample2D conv      -> 256x256 tile
     (2, 63, 41, 256, 0, 512, 3, 2, 1, None),        # odd sizes, stride 2  -> 256x256 tile
     (3, 40, 40, 128, 128, 128, 1, 1, 0, None),      # 1x1 concat shortcut  -> 256x128 tile
+    (2, 48, 48, 96, 32, 128, 3, 1, 1, None),        # channels % 32 only   -> ring path only (BK 32)
+    (1, 16, 16, 1280, 1280, 1280, 3, 1, 1, None),   # long K, few tiles    -> split-K
 ])
 def test_conv_large(device, tiles, case):
     dt = torch.bfloat16
