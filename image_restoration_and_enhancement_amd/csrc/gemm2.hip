@@ -32,7 +32,8 @@ typedef __attribute__((address_space(3))) void lds_void;
 struct Split {
   int splits = 1;      // K splits (gridDim.y = batch * splits)
   int per = 0;         // K steps per split
-  float* ws = nullptr; // fp32 partials [batch*splits][M][N]
+  float* ws = nullptr; // fp32 partials [batch*splits][Mp][Np] (M, N rounded up to the tile: unchecked stores)
+  int Mp = 0, Np = 0;
 };
 
 // Wait until at most n of this wave's vector-memory operations (here: LDS-DMA pieces) are outstanding.
@@ -257,18 +258,14 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
   }
   // ---- split-K: raw fp32 partial tile, epilogue applied by splitk_reduce_kernel
   if (sp.splits > 1) {
-    float* P = sp.ws + (long)blockIdx.y * a.M * a.N;
+    float* P = sp.ws + (long)blockIdx.y * sp.Mp * sp.Np + (long)(m0 + wm * TM * 16 + fgrp * 4) * sp.Np + n0 +
+               wn * TN * 16 + frow;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * TN * 16 + j * 16 + frow;
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * TM * 16 + i * 16 + fgrp * 4 + r;
-          if (m < a.M && n < a.N) P[(long)m * a.N + n] = acc[i][j][r];
-        }
-      }
+        for (int r = 0; r < 4; ++r) P[(long)(i * 16 + r) * sp.Np + j * 16] = acc[i][j][r];
     return;
   }
 
@@ -281,9 +278,10 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
       // adding the residual and applying out_scale, or (GEGLU) combining each 64-wide value block with its
       // gate block h * gelu(g) and writing half-width rows.
       static_assert(BM * BN * 2 <= SMEM * 16, "epilogue tile must fit the staging LDS");
+      // (kept small on purpose: this straight-line part is unrolled over every accumulator; anything
+      //  per-element beyond an FMA and an optional row add goes to the looped pass 2)
       uint16_t* tileS = (uint16_t*)smem;
       uint16_t* Cp = (uint16_t*)a.C + (long)z * a.sC;
-      const int act1 = a.geglu ? (int)ACT_NONE : a.act;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = wn * TN * 16 + j * 16 + frow;
@@ -293,12 +291,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = wm * TM * 16 + i * 16 + fgrp * 4 + r;
-            float v = acc[i][j][r] * a.alpha + bias;
-            if (a.rowadd) {
-              const int m = m0 + row;
-              if (m < a.M && n0 + col < a.N) v += a.rowadd[(long)(m / a.rows_per_group) * a.rowadd_ld + n0 + col];
-            }
-            tileS[row * BN + (((col >> 3) ^ (row & 7)) << 3) + (col & 7)] = f2bf(apply_act(v, act1));
+            tileS[row * BN + (((col >> 3) ^ (row & 7)) << 3) + (col & 7)] = f2bf(acc[i][j][r] * a.alpha + bias);
           }
       }
       __syncthreads();
@@ -306,6 +299,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
       if (a.geglu) {
         // tile columns come in (64 value, 64 gate) pairs; output feature block = n0/2 + 64*pair
         constexpr int OCPR = CPR / 2;
+#pragma unroll 1
         for (int idx = tid; idx < BM * OCPR; idx += 512) {
           const int row = idx / OCPR, oc = idx - row * OCPR;
           const int m = m0 + row;
@@ -320,14 +314,20 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
         }
         return;
       }
+#pragma unroll 1
       for (int idx = tid; idx < BM * CPR; idx += 512) {
         const int row = idx / CPR, c = idx - row * CPR;
         const int m = m0 + row, n = n0 + c * 8;
         if (m >= a.M || n >= a.N) continue;
         uint4 u = *(const uint4*)(tileS + row * BN + ((c ^ (row & 7)) << 3));
-        if (Rp || a.out_scale != 1.f) {
+        if (Rp || a.rowadd || a.out_scale != 1.f) {
           float f[8];
           Vec16<bf16_t>::unpack(u, f);
+          if (a.rowadd) {   // per-image time-embedding projection (added after the bf16 rounding of pass 1)
+            const float4* ra = (const float4*)(a.rowadd + (long)(m / a.rows_per_group) * a.rowadd_ld + n);
+            const float4 x = ra[0], y = ra[1];
+            f[0] += x.x; f[1] += x.y; f[2] += x.z; f[3] += x.w; f[4] += y.x; f[5] += y.y; f[6] += y.z; f[7] += y.w;
+          }
           if (Rp) {
             float rv[8];
             Vec16<bf16_t>::unpack(*(const uint4*)(Rp + (long)m * a.ldr + n), rv);
@@ -354,11 +354,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * TM * 16 + i * 16 + fgrp * 4 + r;
         if (m >= a.M) continue;
-        float v = acc[i][j][r] * a.alpha + bias;
-        if (a.rowadd) v += a.rowadd[(long)(m / a.rows_per_group) * a.rowadd_ld + n];
-        v = apply_act(v, a.act);
-        if (Rp) v += bf2f(Rp[(long)m * a.ldr + n]);
-        v *= a.out_scale;
+        const float v = (acc[i][j][r] * a.alpha + bias) * a.out_scale;   // (no row add / residual here: eligible())
         if constexpr (OUTF32) ((float*)a.C)[(long)z * a.sC + (long)m * a.ldc + n] = v;
         else ((uint16_t*)a.C)[(long)z * a.sC + (long)m * a.ldc + n] = f2bf(v);
       }
@@ -368,7 +364,8 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
 
 // sum of split-K partials + the full epilogue, 8 outputs (one 16-byte bf16 chunk) per thread
 template <bool OUTF32>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const float* __restrict__ ws, int splits) {
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const float* __restrict__ ws, int splits,
+                                                            int Mp, int Np) {
   const int nv = a.N / 8;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)a.M * nv) return;
@@ -378,7 +375,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
 #pragma unroll
   for (int e = 0; e < 8; ++e) f[e] = 0.f;
   for (int s = 0; s < splits; ++s) {
-    const float4* p = (const float4*)(ws + ((long)(z * splits + s) * a.M + m) * a.N + n);
+    const float4* p = (const float4*)(ws + ((long)(z * splits + s) * Mp + m) * Np + n);
     const float4 x = p[0], y = p[1];
     f[0] += x.x; f[1] += x.y; f[2] += x.z; f[3] += x.w; f[4] += y.x; f[5] += y.y; f[6] += y.z; f[7] += y.w;
   }
@@ -429,8 +426,8 @@ void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
   if (sp.splits > 1) {
     const long n = (long)a.M * (a.N / 8);
     dim3 g2((unsigned)((n + 255) / 256), a.batch);
-    if (a.out_f32) splitk_reduce_kernel<true><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits);
-    else splitk_reduce_kernel<false><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits);
+    if (a.out_f32) splitk_reduce_kernel<true><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits, sp.Mp, sp.Np);
+    else splitk_reduce_kernel<false><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits, sp.Mp, sp.Np);
     IRX_LAUNCH_CHECK();
   }
 }
@@ -489,8 +486,18 @@ float* internal_ws(size_t bytes) {
   return g_ws;
 }
 
+bool vec_ok(const GemmArgs& a) {
+  return !a.out_f32 && a.N % 8 == 0 && a.ldc % 8 == 0 && ((uintptr_t)a.C % 16) == 0 &&
+         (!a.residual || (a.ldr % 8 == 0 && ((uintptr_t)a.residual % 16) == 0)) &&
+         (a.batch == 1 || (a.sC % 8 == 0 && (!a.residual || a.sR % 8 == 0)));
+}
+
 bool eligible(const GemmArgs& a) {
   const int bk = step_k();
+  if (a.act != ACT_NONE) return false;   // activations are fused by the 4-wave kernel only (tiny GEMMs)
+  // the unrolled scalar (non-16-byte) epilogue only scales and adds bias: row add / residual need vec rows
+  if (!vec_ok(a) && (a.rowadd || a.residual)) return false;
+  if (a.rowadd && (a.rowadd_ld % 4 != 0 || ((uintptr_t)a.rowadd % 16) != 0)) return false;
   if (a.dtype != BF16 || a.K % bk != 0 || a.ldb % 8 != 0) return false;
   if ((long)a.M * a.batch < 512) return false;     // tiny outputs: the 64x64 4-wave tiles waste less
   if (a.geglu && (a.out_f32 || a.residual || a.batch != 1 || a.N % 128 != 0)) return false;
@@ -498,11 +505,6 @@ bool eligible(const GemmArgs& a) {
   return a.lda % 8 == 0 && (a.batch == 1 || a.sA % 8 == 0);
 }
 
-bool vec_ok(const GemmArgs& a) {
-  return !a.out_f32 && a.N % 8 == 0 && a.ldc % 8 == 0 && ((uintptr_t)a.C % 16) == 0 &&
-         (!a.residual || (a.ldr % 8 == 0 && ((uintptr_t)a.residual % 16) == 0)) &&
-         (a.batch == 1 || (a.sC % 8 == 0 && (!a.residual || a.sR % 8 == 0)));
-}
 
 }  // namespace
 
@@ -518,7 +520,8 @@ size_t gemm_workspace_bytes(const GemmArgs& a) {
   if (!g_large_tiles || !eligible(a)) return 0;
   const Choice c = choose(a);
   if (c.BM == 0 || c.splits <= 1) return 0;
-  return (size_t)c.splits * a.batch * a.M * a.N * sizeof(float);
+  return (size_t)c.splits * a.batch * ((a.M + c.BM - 1) / c.BM * c.BM) * ((a.N + c.BN - 1) / c.BN * c.BN) *
+         sizeof(float);
 }
 
 // Returns false (caller uses the 4-wave kernel) when the shape does not fit the large-tile path.
@@ -536,7 +539,9 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   if (c.splits > 1) {
     if (!b.vec_epilogue && !a.out_f32) return false;     // reduce kernel needs 16-byte output rows
     if (a.out_f32 && (a.ldc % 8 != 0 || a.N % 8 != 0)) return false;
-    const size_t need = (size_t)c.splits * a.batch * a.M * a.N * sizeof(float);
+    sp.Mp = (a.M + c.BM - 1) / c.BM * c.BM;
+    sp.Np = (a.N + c.BN - 1) / c.BN * c.BN;
+    const size_t need = (size_t)c.splits * a.batch * sp.Mp * sp.Np * sizeof(float);
     sp.ws = (a.splitk_ws && a.splitk_ws_bytes >= need) ? (float*)a.splitk_ws : internal_ws(need);
   } else {
     sp.per = a.K / step_k();
