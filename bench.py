@@ -129,6 +129,7 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], help="irx_set_option name=value (A/B experiments)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     args = ap.parse_args()
 
@@ -138,6 +139,9 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     L.load()
+    for o in args.opt:
+        k, v = o.split("=")
+        L.call("irx_set_option", k.encode(), int(v))
 
     cfg = PipelineConfig.default("denoise")
     cfg.scheduler.kind = "ddim"          # BASELINE.json: "50 DDIM steps" (explicit override of the saved PNDM)

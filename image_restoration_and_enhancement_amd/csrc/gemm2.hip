@@ -166,11 +166,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
     for (int j = 0; j < IPW; ++j) {
       const uint16_t* src = rb[j] ? rb[j] + ((isA[j] ? koffA : koffB) + lk[j]) : zp;
       uint4* dst = live[j] ? sbase + (wave * IPW + j) * 64 : smem + SMEM - 64;
-      if constexpr (S == 2) {
-        __builtin_amdgcn_global_load_lds(src, (lds_void*)dst, 16, 0, 0);
-      } else {
-        glds16_asm(src, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
-      }
+      glds16_asm(src, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
     }
     if constexpr (CONV) {
       kc += BK;
@@ -439,15 +435,16 @@ struct Choice {
   int BM = 0, BN = 0, splits = 1, per = 0;
 };
 
-int step_k() { return g_gemm_deep ? 32 : 64; }   // K depth of one pipeline stage
+int step_k() { return g_gemm_deep == 1 ? 32 : 64; }   // K depth of one pipeline stage
 
 Choice choose(const GemmArgs& a) {
   Choice best;
   const int nk = a.K / step_k();
   double best_score = -1.0;
-  const int cands[5][2] = {{256, 256}, {128, 320}, {256, 128}, {128, 256}, {128, 128}};
+  const int cands[6][2] = {{256, 256}, {128, 320}, {256, 128}, {128, 256}, {128, 128}, {256, 160}};
   for (auto& c : cands) {
     const int BM = c[0], BN = c[1];
+    if (BN == 160 && g_gemm_deep != 2) continue;
     if (a.N % BN != 0) continue;
     if (a.geglu && BN % 128 != 0) continue;      // tiles must hold whole (value, gate) block pairs
     const long tiles = (long)((a.M + BM - 1) / BM) * (a.N / BN) * a.batch;
@@ -508,7 +505,7 @@ bool eligible(const GemmArgs& a) {
 
 }  // namespace
 
-bool g_gemm_deep = false;  // irx_set_option("gemm_deep", 1): S-stage BK=32 ring (measured slower; A/B tests)
+int g_gemm_deep = 0;   // irx_set_option("gemm_deep", m): 0 two-stage BK 64, 1 BK-32 ring, 2 BK-64 3/4-stage ring
 int g_gemm_dbg = 0;   // irx_set_option("gemm_deep", 0): 2-stage BK=64 loop (A/B tests)
 
 bool gemm_geglu_fusable(const GemmArgs& a) {
@@ -546,7 +543,17 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   } else {
     sp.per = a.K / step_k();
   }
-  if (g_gemm_deep) {
+  if (g_gemm_deep == 2) {   // BK 64; a third (fourth) stage wherever it fits in 160 KiB
+    switch (c.BM * 1000 + c.BN) {
+      case 256256: launch2<256, 256, 2, 4, 64, 2>(b, sp, s); break;
+      case 128320: launch2<128, 320, 2, 4, 64, 2>(b, sp, s); break;
+      case 256128: launch2<256, 128, 4, 2, 64, 3>(b, sp, s); break;
+      case 128256: launch2<128, 256, 2, 4, 64, 3>(b, sp, s); break;
+      case 128128: launch2<128, 128, 2, 4, 64, 4>(b, sp, s); break;
+      case 256160: launch2<256, 160, 4, 2, 64, 3>(b, sp, s); break;
+      default: return false;
+    }
+  } else if (g_gemm_deep == 1) {
     switch (c.BM * 1000 + c.BN) {
       case 256256: launch2<256, 256, 2, 4, 32, 4>(b, sp, s); break;
       case 128320: launch2<128, 320, 2, 4, 32, 5>(b, sp, s); break;

@@ -47,8 +47,8 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path
 size_t gemm_workspace_bytes(const GemmArgs& a);           // split-K partial buffer the call will use
 bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can apply the GEGLU epilogue
 extern bool g_large_tiles;
-extern bool g_gemm_deep;
-extern int g_gemm_dbg;     // timing diagnostics only: results are wrong when set   // large-tile path: S-stage BK=32 LDS-DMA ring (else 2-stage BK=64)
+extern int g_gemm_deep;    // large-tile pipeline: 0 two-stage BK 64, 1 BK-32 S-stage ring, 2 BK-64 deeper ring
+extern int g_gemm_dbg;     // timing diagnostics only: results are wrong when set
 
 // ------------------------------------------------------------ normalisation
 // GroupNorm over NHWC (optionally a channel concat of two sources). Writes the normalised (and

@@ -68,7 +68,7 @@ def main():
     L.load()
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
-    variants = [("deep", (1, 1)), ("2stage", (1, 0)), ("4wave", (0, 1))]
+    variants = [("s2", (1, 0)), ("ring64", (1, 2)), ("ring32", (1, 1))]
     if args.only in ("", "conv"):
         for lab, N, H, W, C0, C1, Co, k, s, up in CONVS:
             x0 = torch.randn(N, H, W, C0, device=dev, generator=g).to(dt)

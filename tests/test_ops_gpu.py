@@ -209,7 +209,7 @@ def test_geglu(device, dt):
 
 
 # ------------------------------------------------------------------ large-tile (8-wave LDS-DMA) path
-@pytest.fixture(params=[(1, 1), (1, 0), (0, 1)], ids=["deep_ring", "two_stage", "4wave"])
+@pytest.fixture(params=[(1, 0), (1, 1), (1, 2), (0, 0)], ids=["two_stage", "ring32", "ring64", "4wave"])
 def tiles(request):
     from image_restoration_and_enhancement_amd import _lib as L
     L.call("irx_set_option", b"large_tiles", request.param[0])
