@@ -61,6 +61,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "attn_v2") g_attn_v2 = value != 0;
   else if (n == "gemm_deep") g_gemm_deep = value;
   else if (n == "gemm_dbg") g_gemm_dbg = value;
+  else if (n == "gn_v2") g_gn_v2 = value != 0;
   else throw Error("unknown option " + n);
   IRX_API_END
 }

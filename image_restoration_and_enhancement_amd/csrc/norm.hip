@@ -78,6 +78,115 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x0,
   }
 }
 
+__device__ unsigned g_gn_arrivals[4096];   // per-image arrival counters of gn_stats2 (self-resetting)
+
+// GroupNorm statistics without LDS atomics, finalised in-kernel.  Pass 1: thread (16-byte channel vector,
+// pixel row r) accumulates shifted fp32 sums over its pixels and parks (shift, sum, sum of squares) per
+// channel in LDS.  Pass 2: one thread per group expands and merges them in fp64 and writes the chunk
+// partial.  The last chunk block of each image to arrive (agent-scope release/acquire around an arrival
+// counter) folds the image's partials into (mean, rstd) — no separate finalize launch.
+template <typename T>
+__global__ __launch_bounds__(256) void gn_stats2_kernel(const T* __restrict__ x0, const T* __restrict__ x1, int C0,
+                                                        int C1, int HW, int G, int cpix, double* part, float cnt_all,
+                                                        float eps, float2* __restrict__ mr) {
+  constexpr int VEC = 16 / (int)sizeof(T);
+  extern __shared__ float tri[];               // [3][rows][C]: shift, sum, sum of squares
+  __shared__ double red[2][256];
+  __shared__ int last;
+  const int C = C0 + C1;
+  const int nv = C / VEC;
+  const int cg = C / G;
+  const int n = blockIdx.y, chunk = blockIdx.x, nch = gridDim.x;
+  const int p0 = chunk * cpix, p1 = min(HW, p0 + cpix);
+  const int rows = nv >= 256 ? 1 : 256 / nv;
+  const int r = threadIdx.x / (nv >= 256 ? 256 : nv);
+  float* X0 = tri;
+  float* S = tri + rows * C;
+  float* Q = tri + 2 * rows * C;
+  for (int vb = 0; vb < nv; vb += 256) {
+    const int v = vb + (nv >= 256 ? threadIdx.x : threadIdx.x % nv);
+    if (v >= nv || r >= rows) continue;
+    const int c = v * VEC;
+    const T* src = c < C0 ? x0 + c : x1 + (c - C0);
+    const int ld = c < C0 ? C0 : C1;
+    float s[VEC], q[VEC], xs[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) { s[e] = 0.f; q[e] = 0.f; xs[e] = 0.f; }
+    if (p0 + r < p1) Vec16<T>::unpack(*(const uint4*)(src + ((long)n * HW + p0 + r) * ld), xs);
+    for (int p = p0 + r; p < p1; p += rows) {
+      float f[VEC];
+      Vec16<T>::unpack(*(const uint4*)(src + ((long)n * HW + p) * ld), f);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float dv = f[e] - xs[e];
+        s[e] += dv;
+        q[e] = fmaf(dv, dv, q[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      X0[r * C + c + e] = xs[e];
+      S[r * C + c + e] = s[e];
+      Q[r * C + c + e] = q[e];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < G) {
+    const int g = threadIdx.x;
+    double sd = 0.0, qd = 0.0;
+    for (int rr = 0; rr < rows; ++rr) {
+      const int first = p0 + rr;
+      const double cnt = first < p1 ? (double)((p1 - first + rows - 1) / rows) : 0.0;
+      for (int c = g * cg; c < (g + 1) * cg; ++c) {
+        const double xv = X0[rr * C + c], sv = S[rr * C + c];
+        sd += cnt * xv + sv;
+        qd += cnt * xv * xv + 2.0 * xv * sv + (double)Q[rr * C + c];
+      }
+    }
+    double* o = part + (((long)n * nch + chunk) * G + g) * 2;
+    o[0] = sd;
+    o[1] = qd;
+  }
+  // ---- publish this chunk; the image's last arriving block finalises
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(&g_gn_arrivals[n], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (unsigned)(nch - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  // threads t = g + G*j sum chunks j, j + 256/G, ...
+  const int per = 256 / G;
+  const int g = threadIdx.x % G, j = threadIdx.x / G;
+  double sd = 0.0, qd = 0.0;
+  if (j < per)
+    for (int ch = j; ch < nch; ch += per) {
+      const double* o = part + (((long)n * nch + ch) * G + g) * 2;
+      sd += o[0];
+      qd += o[1];
+    }
+  red[0][threadIdx.x] = sd;
+  red[1][threadIdx.x] = qd;
+  __syncthreads();
+  if (threadIdx.x < G) {
+    double a = 0.0, b = 0.0;
+    for (int jj = 0; jj < per; ++jj) { a += red[0][threadIdx.x + G * jj]; b += red[1][threadIdx.x + G * jj]; }
+    const double cnt = (double)cnt_all;
+    const double mean = a / cnt;
+    double var = b / cnt - mean * mean;
+    if (var < 0.0) var = 0.0;
+    mr[n * G + threadIdx.x] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+  }
+  if (threadIdx.x == 0) g_gn_arrivals[n] = 0u;   // ready for the next call on this stream
+}
+
 // per (image, group): fold the chunk partials into (mean, rstd) once
 __global__ __launch_bounds__(64) void gn_finalize_kernel(const double* __restrict__ part, int nchunk, int G,
                                                          double cnt, float eps, float2* __restrict__ mr) {
@@ -204,11 +313,20 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
   double* part = (double*)ws;
   float2* mr = (float2*)(part + (size_t)N * nch * G * 2);
   const int C = C0 + C1;
-  gn_stats_kernel<T><<<dim3(nch, N), 256, 0, s>>>((const T*)x0, (const T*)x1, C0, C1, HW, G, chunk_pix(HW), part);
-  IRX_LAUNCH_CHECK();
-  gn_finalize_kernel<<<N, 64, 0, s>>>(part, nch, G, (double)HW * (C / G), eps, mr);
-  IRX_LAUNCH_CHECK();
   const int VEC = 16 / (int)sizeof(T);
+  if (g_gn_v2 && N <= 4096) {
+    const int nvv = C / VEC;
+    const int rws = nvv >= 256 ? 1 : 256 / nvv;
+    gn_stats2_kernel<T><<<dim3(nch, N), 256, 3 * rws * C * sizeof(float), s>>>(
+        (const T*)x0, (const T*)x1, C0, C1, HW, G, chunk_pix(HW), part, (float)HW * (C / G), eps, mr);
+    IRX_LAUNCH_CHECK();
+  } else {
+    gn_stats_kernel<T><<<dim3(nch, N), 256, 0, s>>>((const T*)x0, (const T*)x1, C0, C1, HW, G, chunk_pix(HW),
+                                                    part);
+    IRX_LAUNCH_CHECK();
+    gn_finalize_kernel<<<N, 64, 0, s>>>(part, nch, G, (double)HW * (C / G), eps, mr);
+    IRX_LAUNCH_CHECK();
+  }
   // ~16 pixels per thread per block, one fixed channel chunk per thread
   const int nv = C / VEC;
   const int rows = nv >= 256 ? 1 : 256 / nv;
@@ -233,6 +351,8 @@ void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamm
 }
 
 }  // namespace
+
+bool g_gn_v2 = true;   // irx_set_option("gn_v2", 0): LDS-atomic stats + separate finalize (A/B)
 
 size_t gn_ws_bytes(int N, int HW, int G) {
   return (size_t)N * n_chunks(HW) * G * 2 * sizeof(double) + (size_t)N * G * sizeof(float2);
