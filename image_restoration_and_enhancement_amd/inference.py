@@ -82,7 +82,11 @@ def _resolve_pretrained(repo_id: str) -> Path:
 class RestorationPipeline:
     """Unified restoration pipeline (reference `src/inference.py:48-890`) on the native MI355X engine."""
 
-    def __init__(self, device: str = "auto", config: dict | None = None, seed: int = 42):
+    def __init__(self, device: str = "auto", config: dict | None = None, seed: int = 42, backend: str | None = None):
+        # `backend` is accepted (and ignored) because the reference's own prediction driver passes it
+        # (scripts/generate_predictions.py:18), which the reference constructor rejects with a TypeError.
+        if backend is not None:
+            logger.info(f"backend={backend!r} ignored (per-task backends come from config)")
         if device == "auto":
             self.device = "cuda" if torch.cuda.is_available() else "cpu"
         else:

@@ -166,3 +166,27 @@ def test_nl_means_reduces_noise():
     noisy = clean + rng.normal(0, 8, clean.shape)
     out = CL.nl_means(noisy, np.array([10.0, 10.0, 10.0]), 7, 11)
     assert np.abs(out - clean).mean() < 0.5 * np.abs(noisy - clean).mean()
+
+
+def test_prediction_driver_layout(tmp_path):
+    """scripts/generate_predictions.py keeps the reference's {task}/{split}/<name> layout (CPU: fallbacks)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = tmp_path / "pairs"
+    rng = np.random.default_rng(3)
+    for task in ("denoise", "sr_x4", "colorize", "inpaint"):
+        d = root / task / "test" / "input"
+        d.mkdir(parents=True)
+        Image.fromarray(rng.integers(0, 256, (16, 16, 3), dtype=np.uint8)).save(d / "a.png")
+    (root / "inpaint" / "test" / "mask").mkdir()
+    Image.new("L", (16, 16), 255).save(root / "inpaint" / "test" / "mask" / "a.png")
+    out = tmp_path / "pred"
+    script = Path(__file__).resolve().parents[1] / "scripts" / "generate_predictions.py"
+    r = subprocess.run([sys.executable, str(script), "--test_root", str(root), "--output_root", str(out)],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=600,
+                       env={**__import__("os").environ, "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert Image.open(out / "denoise" / "test" / "a.png").size == (16, 16)
+    assert Image.open(out / "sr_x4" / "test" / "a.png").size == (64, 64)
+    assert (out / "colorize" / "test" / "a.png").exists() and (out / "inpaint" / "test" / "a.png").exists()
