@@ -61,17 +61,18 @@ __device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds_addr) {
 // S == 2 is the classic double buffer (drain + barrier per step); S > 2 keeps S-2 stages of LDS-DMA in
 // flight across each (raw) barrier, waiting with a counted vmcnt for exactly the stage about to be read.
 template <int BM, int BN, int WM, int WN, int BK, int S, bool CONV, bool OUTF32, bool RESIZE>
-__global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
+__global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kernel(GemmArgs a, Split sp) {
+  constexpr int NW = WM * WN, NT = NW * 64;   // 8 waves (1 block/CU) or 4 waves (2 blocks/CU)
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int ROWS = BM + BN;
   constexpr int CPR = BK / 8;                // 16-byte chunks per row per stage
   constexpr int RPI = 64 / CPR;              // rows per 1 KiB LDS-DMA wave instruction
   constexpr int NINST = ROWS / RPI;          // wave instructions per stage
-  constexpr int IPW = (NINST + 7) / 8;       // per wave (the surplus ones are dummies into a scratch KiB)
+  constexpr int IPW = (NINST + NW - 1) / NW;  // per wave (the surplus ones are dummies into a scratch KiB)
   constexpr int STAGE = ROWS * CPR;          // uint4 per stage
   constexpr int KSUB = BK / 32;              // 32-deep MFMA sub-steps per stage
-  static_assert(WM * WN == 8 && ROWS % RPI == 0 && BM % 16 == 0 && (BK == 32 || BK == 64), "tile shape");
-  constexpr int SMEM = (S * STAGE > BM * BN / 8 ? S * STAGE : BM * BN / 8) + (NINST % 8 ? 64 : 0);
+  static_assert((NW == 8 || NW == 4) && ROWS % RPI == 0 && BM % 16 == 0 && (BK == 32 || BK == 64), "tile shape");
+  constexpr int SMEM = (S * STAGE > BM * BN / 8 ? S * STAGE : BM * BN / 8) + (NINST % NW ? 64 : 0);
   __shared__ __attribute__((aligned(16))) uint4 smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
         // tile columns come in (64 value, 64 gate) pairs; output feature block = n0/2 + 64*pair
         constexpr int OCPR = CPR / 2;
 #pragma unroll 1
-        for (int idx = tid; idx < BM * OCPR; idx += 512) {
+        for (int idx = tid; idx < BM * OCPR; idx += NT) {
           const int row = idx / OCPR, oc = idx - row * OCPR;
           const int m = m0 + row;
           const int hc = (oc >> 3) * 16 + (oc & 7);       // value chunk; gate chunk is hc + 8
@@ -311,7 +312,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs a, Split sp) {
         return;
       }
 #pragma unroll 1
-      for (int idx = tid; idx < BM * CPR; idx += 512) {
+      for (int idx = tid; idx < BM * CPR; idx += NT) {
         const int row = idx / CPR, c = idx - row * CPR;
         const int m = m0 + row, n = n0 + c * 8;
         if (m >= a.M || n >= a.N) continue;
@@ -400,7 +401,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
 template <int BM, int BN, int WM, int WN, int BK, int S>
 void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles, a.batch * sp.splits), block(512);
+  dim3 grid(tiles, a.batch * sp.splits), block(WM * WN * 64);
   const bool rs = a.conv && (a.g.Hv != a.g.Hin || a.g.Wv != a.g.Win);
   std::string nm;
   if (prof_on())   // same spelling as the demangled name rocprofv3 reports
@@ -433,6 +434,8 @@ constexpr int kCUs = 256;
 
 struct Choice {
   int BM = 0, BN = 0, splits = 1, per = 0;
+  bool small = false;   // 4-wave block, two resident per CU (short-K GEMMs: one block's prologue/epilogue
+                        // overlaps the other's MFMA loop)
 };
 
 int step_k() { return g_gemm_deep == 1 ? 32 : 64; }   // K depth of one pipeline stage
@@ -440,6 +443,13 @@ int step_k() { return g_gemm_deep == 1 ? 32 : 64; }   // K depth of one pipeline
 Choice choose(const GemmArgs& a) {
   Choice best;
   const int nk = a.K / step_k();
+  if (g_gemm_small && g_gemm_deep == 0 && a.K <= g_gemm_small_kmax) {
+    const int bn = (!a.geglu && a.N % 160 == 0) ? 160 : (a.N % 128 == 0 ? 128 : 0);
+    if (bn) {
+      best.BM = 128; best.BN = bn; best.small = true; best.splits = 1; best.per = nk;
+      return best;
+    }
+  }
   double best_score = -1.0;
   const int cands[6][2] = {{256, 256}, {128, 320}, {256, 128}, {128, 256}, {128, 128}, {256, 160}};
   for (auto& c : cands) {
@@ -506,7 +516,9 @@ bool eligible(const GemmArgs& a) {
 }  // namespace
 
 int g_gemm_deep = 0;   // irx_set_option("gemm_deep", m): 0 two-stage BK 64, 1 BK-32 ring, 2 BK-64 3/4-stage ring
-int g_gemm_dbg = 0;   // irx_set_option("gemm_deep", 0): 2-stage BK=64 loop (A/B tests)
+int g_gemm_dbg = 0;
+bool g_gemm_small = false;   // irx_set_option("gemm_small", 1): 4-wave 128x160 / 128x128 tiles for K <= kmax
+int g_gemm_small_kmax = 1280;
 
 bool gemm_geglu_fusable(const GemmArgs& a) {
   if (!g_large_tiles || !a.geglu || !eligible(a) || !vec_ok(a)) return false;
@@ -543,7 +555,10 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   } else {
     sp.per = a.K / step_k();
   }
-  if (g_gemm_deep == 2) {   // BK 64; a third (fourth) stage wherever it fits in 160 KiB
+  if (c.small) {
+    if (c.BN == 160) launch2<128, 160, 2, 2, 64, 2>(b, sp, s);
+    else launch2<128, 128, 2, 2, 64, 2>(b, sp, s);
+  } else if (g_gemm_deep == 2) {   // BK 64; a third (fourth) stage wherever it fits in 160 KiB
     switch (c.BM * 1000 + c.BN) {
       case 256256: launch2<256, 256, 2, 4, 64, 2>(b, sp, s); break;
       case 128320: launch2<128, 320, 2, 4, 64, 2>(b, sp, s); break;

@@ -49,6 +49,8 @@ bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can
 extern bool g_large_tiles;
 extern int g_gemm_deep;    // large-tile pipeline: 0 two-stage BK 64, 1 BK-32 S-stage ring, 2 BK-64 deeper ring
 extern int g_gemm_dbg;     // timing diagnostics only: results are wrong when set
+extern bool g_gemm_small;  // short-K GEMMs on 4-wave 128x160 / 128x128 tiles, 2 blocks per CU
+extern int g_gemm_small_kmax;
 
 // ------------------------------------------------------------ normalisation
 // GroupNorm over NHWC (optionally a channel concat of two sources). Writes the normalised (and

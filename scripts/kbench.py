@@ -68,7 +68,7 @@ def main():
     L.load()
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
-    variants = [("s2", (1, 0)), ("ring64", (1, 2)), ("ring32", (1, 1))]
+    variants = [("s2", (1, 0, 0)), ("ring64", (1, 2, 0)), ("small", (1, 0, 1))]
     if args.only in ("", "conv"):
         for lab, N, H, W, C0, C1, Co, k, s, up in CONVS:
             x0 = torch.randn(N, H, W, C0, device=dev, generator=g).to(dt)
@@ -78,9 +78,10 @@ def main():
             Ho, Wo = up if up else (H, W)
             flops = 2.0 * N * Ho * Wo * Co * (C0 + C1) * k * k
             res = []
-            for vn, (lt, dp) in variants:
+            for vn, (lt, dp, sm) in variants:
                 L.call("irx_set_option", b"large_tiles", lt)
                 L.call("irx_set_option", b"gemm_deep", dp)
+                L.call("irx_set_option", b"gemm_small", sm)
                 ms = timeit(lambda: O.conv2d(x0, w, b, x1=x1, up_hw=up), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             print(f"{lab:24s} " + " | ".join(res), flush=True)
@@ -90,14 +91,16 @@ def main():
             Bw = (torch.randn(N, K, device=dev, generator=g) / math.sqrt(K)).to(dt)
             flops = 2.0 * M * N * K
             res = []
-            for vn, (lt, dp) in variants:
+            for vn, (lt, dp, sm) in variants:
                 L.call("irx_set_option", b"large_tiles", lt)
                 L.call("irx_set_option", b"gemm_deep", dp)
+                L.call("irx_set_option", b"gemm_small", sm)
                 ms = timeit(lambda: O.gemm(A, Bw), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             print(f"{lab:24s} " + " | ".join(res), flush=True)
     L.call("irx_set_option", b"large_tiles", 1)
     L.call("irx_set_option", b"gemm_deep", 0)
+    L.call("irx_set_option", b"gemm_small", 0)
     if args.only in ("", "attn"):
         for lab, B, Lq, Lk, C in ATTNS:
             q = torch.randn(B, Lq, C, device=dev, generator=g).to(dt)

@@ -209,14 +209,17 @@ def test_geglu(device, dt):
 
 
 # ------------------------------------------------------------------ large-tile (8-wave LDS-DMA) path
-@pytest.fixture(params=[(1, 0), (1, 1), (1, 2), (0, 0)], ids=["two_stage", "ring32", "ring64", "4wave"])
+@pytest.fixture(params=[(1, 0, 0), (1, 1, 0), (1, 2, 0), (1, 0, 1), (0, 0, 0)],
+                ids=["two_stage", "ring32", "ring64", "small4w", "4wave"])
 def tiles(request):
     from image_restoration_and_enhancement_amd import _lib as L
     L.call("irx_set_option", b"large_tiles", request.param[0])
     L.call("irx_set_option", b"gemm_deep", request.param[1])
+    L.call("irx_set_option", b"gemm_small", request.param[2])
     yield request.param
     L.call("irx_set_option", b"large_tiles", 1)
     L.call("irx_set_option", b"gemm_deep", 0)
+    L.call("irx_set_option", b"gemm_small", 0)
 
 
 @pytest.mark.parametrize("case", [
