@@ -201,7 +201,7 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
       const float mnew = fmaxf(mrow[qt], tmax);
       const bool none = mnew == -INFINITY;           // every key so far masked
-      const float alpha = none ? 1.f : exp2f((mrow[qt] - mnew) * sl2);
+      const float alpha = none ? 1.f : __builtin_amdgcn_exp2f((mrow[qt] - mnew) * sl2);
       const float nb = none ? 0.f : -mnew * sl2;
       mrow[qt] = mnew;
       float lsum = 0.f;
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
         float p[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          p[i] = exp2f(fmaf(s[kt][qt][i], sl2, nb));
+          p[i] = __builtin_amdgcn_exp2f(fmaf(s[kt][qt][i], sl2, nb));
           lsum += p[i];
         }
         if constexpr (sizeof(T) == 2) {
@@ -287,7 +287,9 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
 //   (lane group g holds keys 4g..4g+3 of each), V^T comes from two ds_read_b64_tr_b16 of the same
 //   key sets, so the permuted k order matches on both operands.
 // KT keys per LDS tile (128 at d <= 80, 64 at d = 160 to bound registers); 4 waves x 32 queries.
-template <int DQ, int DV, int KT>
+// ONES: the head dim leaves a zero pad column in V (d < DV); it is set to 1 so the PV MFMAs also produce
+// the softmax row sums (O^T row d = sum_k P[q][k]) and the per-score VALU add disappears.
+template <int DQ, int DV, int KT, bool ONES>
 __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
   constexpr int SK = DQ + 8;                                     // 16 rows x b128 reads conflict-free
   constexpr int SV = ((DV * 2 / 32) % 2 == 1) ? DV : DV + 16;    // 8 rows x 32 B tr reads conflict-free
@@ -310,7 +312,7 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
   const bf16_t* __restrict__ V = (const bf16_t*)a.v + (long)b * a.sv + (long)h * d;
 
   for (int i = tid; i < KT * SK; i += 256) Ks[i] = 0;
-  for (int i = tid; i < KT * SV; i += 256) Vs[i] = 0;
+  for (int i = tid; i < KT * SV; i += 256) Vs[i] = (ONES && i % SV == a.d) ? (bf16_t)0x3F80 : (bf16_t)0;
 
   s16x8 qf[kQT][NDC];
   s16x4 qtail[kQT];
@@ -421,10 +423,10 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
       const float mnew = fmaxf(mrow[qt], tmax);
       const bool none = mnew == -INFINITY;
-      const float alpha = none ? 1.f : exp2f((mrow[qt] - mnew) * sl2);
+      const float alpha = none ? 1.f : __builtin_amdgcn_exp2f((mrow[qt] - mnew) * sl2);
       nbq[qt] = none ? 0.f : -mnew * sl2;
       mrow[qt] = mnew;
-      lrow[qt] *= alpha;
+      if constexpr (!ONES) lrow[qt] *= alpha;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) o[dt][qt] *= alpha;
     }
@@ -440,11 +442,11 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
         for (int half = 0; half < 2; ++half)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float p = exp2f(fmaf(s[2 * c + half][qt][i], sl2, nbq[qt]));
-            lsum += p;
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[2 * c + half][qt][i], sl2, nbq[qt]));
+            if constexpr (!ONES) lsum += p;
             pf[qt][half * 4 + i] = (short)f2bf(p);
           }
-        lrow[qt] += lsum;
+        if constexpr (!ONES) lrow[qt] += lsum;
       }
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
@@ -463,9 +465,19 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
   bf16_t* __restrict__ O = (bf16_t*)a.o + (long)b * a.so + (long)h * d;
 #pragma unroll
   for (int qt = 0; qt < kQT; ++qt) {
-    float l = lrow[qt];
-    l += __shfl_xor(l, 16);
-    l += __shfl_xor(l, 32);
+    float l;
+    if constexpr (ONES) {
+      // row d of O^T: tile dt1 = d/16, lane group (d%16)/4, element d%4 (d % 4 == 0: element 0)
+      float v = 0.f;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+        if (dt == d / 16) v = o[dt][qt][0];
+      l = __shfl(v, li + 16 * ((d % 16) / 4));
+    } else {
+      l = lrow[qt];
+      l += __shfl_xor(l, 16);
+      l += __shfl_xor(l, 32);
+    }
     const float inv = l > 0.f ? 1.f / l : 0.f;
     const int q = q0 + qt * 16 + li;
     if (q >= a.Lq) continue;
@@ -483,14 +495,16 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
 
 void launch_bf16(const AttnArgs& a, hipStream_t s) {
   dim3 grid((a.Lq + kQB - 1) / kQB, a.H, a.B), block(256);
-  const char* inst = a.d == 40 ? "48, 48, 128" : a.d == 64 ? "64, 64, 128" : a.d == 80 ? "80, 80, 64" : "160, 160, 32";
+  const char* inst = a.d == 40 ? "48, 48, 128, true"
+                     : a.d == 64 ? "64, 64, 128, false"
+                     : a.d == 80 ? "80, 80, 64, false" : "160, 160, 32, false";
   ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn2_kernel<") + inst + ">" : std::string(),
                4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
   switch (a.d) {
-    case 40: attn2_kernel<48, 48, 128><<<grid, block, 0, s>>>(a); break;
-    case 64: attn2_kernel<64, 64, 128><<<grid, block, 0, s>>>(a); break;
-    case 80: attn2_kernel<80, 80, 64><<<grid, block, 0, s>>>(a); break;
-    case 160: attn2_kernel<160, 160, 32><<<grid, block, 0, s>>>(a); break;
+    case 40: attn2_kernel<48, 48, 128, true><<<grid, block, 0, s>>>(a); break;
+    case 64: attn2_kernel<64, 64, 128, false><<<grid, block, 0, s>>>(a); break;
+    case 80: attn2_kernel<80, 80, 64, false><<<grid, block, 0, s>>>(a); break;
+    case 160: attn2_kernel<160, 160, 32, false><<<grid, block, 0, s>>>(a); break;
     default: throw Error("attention: unsupported head dim " + std::to_string(a.d));
   }
   IRX_LAUNCH_CHECK();
