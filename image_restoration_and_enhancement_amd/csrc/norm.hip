@@ -314,9 +314,9 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
   float2* mr = (float2*)(part + (size_t)N * nch * G * 2);
   const int C = C0 + C1;
   const int VEC = 16 / (int)sizeof(T);
-  if (g_gn_v2 && N <= 4096) {
-    const int nvv = C / VEC;
-    const int rws = nvv >= 256 ? 1 : 256 / nvv;
+  const int nvv = C / VEC;
+  const int rws = nvv >= 256 ? 1 : 256 / nvv;
+  if (g_gn_v2 && N <= 4096 && 3 * rws * C * sizeof(float) <= 60 * 1024) {   // default dynamic-LDS limit
     gn_stats2_kernel<T><<<dim3(nch, N), 256, 3 * rws * C * sizeof(float), s>>>(
         (const T*)x0, (const T*)x1, C0, C1, HW, G, chunk_pix(HW), part, (float)HW * (C / G), eps, mr);
     IRX_LAUNCH_CHECK();
