@@ -293,10 +293,11 @@ template <int DQ, int DV, int KT, bool ONES>
 __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
   constexpr int SK = DQ + 8;                                     // 16 rows x b128 reads conflict-free
   constexpr int SV = ((DV * 2 / 32) % 2 == 1) ? DV : DV + 16;    // 8 rows x 32 B tr reads conflict-free
-  // QK^T contracts over DQ = 32 * NDC (+ 16 with one 16x16x16 MFMA when DQ % 32 == 16): d = 40 -> 48, 80 -> 80
+  // QK^T contracts over DQ = 32 * NDC (head dim zero-padded).  (A 16x16x16 MFMA for a d % 32 == 8..16 tail was
+  // tried: hipcc (ROCm 7.2) issues it right behind the 16x16x32 producing its accumulator with no wait states,
+  // and the result is wrong — mixed-shape MFMA accumulation chains are avoided here.)
   constexpr int NDC = DQ / 32, NDT = DV / 16, NKT = KT / 16, NKC = KT / 32;
-  constexpr bool TAIL = DQ % 32 == 16;
-  static_assert(DQ % 32 == 0 || DQ % 32 == 16, "head dim padding");
+  static_assert(DQ % 32 == 0, "head dim padding");
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[KT * SK];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[KT * SV];
@@ -315,7 +316,6 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
   for (int i = tid; i < KT * SV; i += 256) Vs[i] = (ONES && i % SV == a.d) ? (bf16_t)0x3F80 : (bf16_t)0;
 
   s16x8 qf[kQT][NDC];
-  s16x4 qtail[kQT];
 #pragma unroll
   for (int qt = 0; qt < kQT; ++qt) {
     const int q = q0 + qt * 16 + li;
@@ -325,11 +325,6 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
       s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
       if (q < a.Lq && e < d) v = *(const s16x8*)(Q + (long)q * a.ldq + e);
       qf[qt][dc] = v;
-    }
-    qtail[qt] = s16x4{0, 0, 0, 0};
-    if constexpr (TAIL) {
-      const int e = NDC * 32 + 4 * g;
-      if (q < a.Lq && e < d) qtail[qt] = *(const s16x4*)(Q + (long)q * a.ldq + e);
     }
   }
   f32x4 o[NDT][kQT];
@@ -392,12 +387,6 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
         for (int qt = 0; qt < kQT; ++qt)
           s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf),
                                                               __builtin_bit_cast(bf16x8, qf[qt][dc]), s[kt][qt], 0, 0, 0);
-      }
-      if constexpr (TAIL) {
-        const s16x4 kf = *(const s16x4*)(Ks + (kt * 16 + li) * SK + NDC * 32 + 4 * g);
-#pragma unroll
-        for (int qt = 0; qt < kQT; ++qt)
-          s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qtail[qt], s[kt][qt], 0, 0, 0);
       }
     }
 
@@ -495,15 +484,18 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
 
 void launch_bf16(const AttnArgs& a, hipStream_t s) {
   dim3 grid((a.Lq + kQB - 1) / kQB, a.H, a.B), block(256);
-  const char* inst = a.d == 40 ? "48, 48, 128, true"
+  const char* inst = a.d == 40 ? (g_attn_d40 == 1 ? "64, 48, 128, false" : "64, 48, 128, true")
                      : a.d == 64 ? "64, 64, 128, false"
-                     : a.d == 80 ? "80, 80, 64, false" : "160, 160, 32, false";
+                     : a.d == 80 ? "96, 80, 64, false" : "160, 160, 32, false";
   ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn2_kernel<") + inst + ">" : std::string(),
                4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
   switch (a.d) {
-    case 40: attn2_kernel<48, 48, 128, true><<<grid, block, 0, s>>>(a); break;
+    case 40:
+      if (g_attn_d40 == 1) attn2_kernel<64, 48, 128, false><<<grid, block, 0, s>>>(a);
+      else attn2_kernel<64, 48, 128, true><<<grid, block, 0, s>>>(a);
+      break;
     case 64: attn2_kernel<64, 64, 128, false><<<grid, block, 0, s>>>(a); break;
-    case 80: attn2_kernel<80, 80, 64, false><<<grid, block, 0, s>>>(a); break;
+    case 80: attn2_kernel<96, 80, 64, false><<<grid, block, 0, s>>>(a); break;
     case 160: attn2_kernel<160, 160, 32, false><<<grid, block, 0, s>>>(a); break;
     default: throw Error("attention: unsupported head dim " + std::to_string(a.d));
   }
@@ -543,5 +535,6 @@ void attention(const AttnArgs& a, hipStream_t s) {
 }
 
 bool g_attn_v2 = true;
+int g_attn_d40 = 0;   // d = 40 variant (A/B): 0 ones-column row sums, 1 VALU row sums
 
 }  // namespace irx

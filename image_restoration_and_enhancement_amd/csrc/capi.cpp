@@ -63,6 +63,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gemm_dbg") g_gemm_dbg = value;
   else if (n == "gn_v2") g_gn_v2 = value != 0;
   else if (n == "gemm_small") g_gemm_small = value != 0;
+  else if (n == "attn_d40") g_attn_d40 = value;
   else if (n == "gemm_small_kmax") g_gemm_small_kmax = value;
   else throw Error("unknown option " + n);
   IRX_API_END

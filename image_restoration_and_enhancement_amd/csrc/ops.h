@@ -76,7 +76,8 @@ struct AttnArgs {
   int causal = 0;
 };
 void attention(const AttnArgs& a, hipStream_t s);
-extern bool g_attn_v2;   // bf16: 16x16x32 kernel (irx_set_option("attn_v2", 0) selects the 16x16x16 one)
+extern bool g_attn_v2;
+extern int g_attn_d40;   // bf16: 16x16x32 kernel (irx_set_option("attn_v2", 0) selects the 16x16x16 one)
 
 // ------------------------------------------------------------ elementwise / data movement
 // out[m][f] = h * gelu_erf(g): h = proj[m][f], g = proj[m][F + f]; with interleave64 the proj columns are
