@@ -279,6 +279,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       //  per-element beyond an FMA and an optional row add goes to the looped pass 2)
       uint16_t* tileS = (uint16_t*)smem;
       uint16_t* Cp = (uint16_t*)a.C + (long)z * a.sC;
+      constexpr int CPR = BN / 8;               // 16-byte chunks per row
+      // chunk swizzle inside whole groups of 8 chunks only (BN = 160 leaves a 4-chunk tail unswizzled)
+      auto csw = [](int c, int row) { return c < (CPR & ~7) ? c ^ (row & 7) : c; };
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = wn * TN * 16 + j * 16 + frow;
@@ -288,11 +291,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = wm * TM * 16 + i * 16 + fgrp * 4 + r;
-            tileS[row * BN + (((col >> 3) ^ (row & 7)) << 3) + (col & 7)] = f2bf(acc[i][j][r] * a.alpha + bias);
+            tileS[row * BN + (csw(col >> 3, row) << 3) + (col & 7)] = f2bf(acc[i][j][r] * a.alpha + bias);
           }
       }
       __syncthreads();
-      constexpr int CPR = BN / 8;               // 16-byte chunks per row
       if (a.geglu) {
         // tile columns come in (64 value, 64 gate) pairs; output feature block = n0/2 + 64*pair
         constexpr int OCPR = CPR / 2;
@@ -316,7 +318,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         const int row = idx / CPR, c = idx - row * CPR;
         const int m = m0 + row, n = n0 + c * 8;
         if (m >= a.M || n >= a.N) continue;
-        uint4 u = *(const uint4*)(tileS + row * BN + ((c ^ (row & 7)) << 3));
+        uint4 u = *(const uint4*)(tileS + row * BN + (csw(c, row) << 3));
         if (Rp || a.rowadd || a.out_scale != 1.f) {
           float f[8];
           Vec16<bf16_t>::unpack(u, f);
