@@ -4,7 +4,7 @@
 # Usage: bash scripts/gpu_measure.sh <tag> [kernel-regex]
 set -e -o pipefail
 TAG=${1:-r01}
-KRE=${2:-gemm2_kernel<128, 320, 2, 4, true, false, false>}
+KRE=${2:-gemm2_kernel<128, 320, 2, 4, 64, 2, true, false, false>}
 O=gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

@@ -63,12 +63,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--ref", action="store_true", help="also time torch (hipBLASLt / MIOpen) on the same shapes")
+    ap.add_argument("--variants", default="s2,ring64,small")
     args = ap.parse_args()
     dev = torch.device("cuda")
     L.load()
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
-    variants = [("s2", (1, 0, 0)), ("ring64", (1, 2, 0)), ("small", (1, 0, 1))]
+    allv = {"s2": (1, 0, 0), "ring64": (1, 2, 0), "small": (1, 0, 1), "4wave": (0, 0, 0)}
+    variants = [(v, allv[v]) for v in args.variants.split(",")]
     if args.only in ("", "conv"):
         for lab, N, H, W, C0, C1, Co, k, s, up in CONVS:
             x0 = torch.randn(N, H, W, C0, device=dev, generator=g).to(dt)
@@ -84,6 +87,14 @@ def main():
                 L.call("irx_set_option", b"gemm_small", sm)
                 ms = timeit(lambda: O.conv2d(x0, w, b, x1=x1, up_hw=up), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
+            if args.ref:   # MIOpen (torch) channels-last bf16 conv on the same data: a known-good reference
+                xr = (torch.cat([x0, x1], -1) if x1 is not None else x0).permute(0, 3, 1, 2)
+                if up:
+                    xr = torch.nn.functional.interpolate(xr, size=up, mode="nearest")
+                xr = xr.contiguous(memory_format=torch.channels_last)
+                wr = w.contiguous(memory_format=torch.channels_last)
+                ms = timeit(lambda: torch.nn.functional.conv2d(xr, wr, None, s, k // 2), args.iters)
+                res.append(f"miopen {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             print(f"{lab:24s} " + " | ".join(res), flush=True)
     if args.only in ("", "gemm"):
         for lab, M, N, K in GEMMS:
@@ -97,6 +108,10 @@ def main():
                 L.call("irx_set_option", b"gemm_small", sm)
                 ms = timeit(lambda: O.gemm(A, Bw), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
+            if args.ref:   # hipBLASLt (torch.matmul) on the same data: a known-good reference
+                Bt = Bw.t()
+                ms = timeit(lambda: torch.matmul(A, Bt), args.iters)
+                res.append(f"hipblaslt {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             print(f"{lab:24s} " + " | ".join(res), flush=True)
     L.call("irx_set_option", b"large_tiles", 1)
     L.call("irx_set_option", b"gemm_deep", 0)
@@ -108,10 +123,15 @@ def main():
             v = torch.randn(B, Lk, C, device=dev, generator=g).to(dt)
             flops = 4.0 * B * Lq * Lk * C
             res = []
-            for vn, v2 in (("v2", 1), ("v1", 0)):
+            for vn, v2 in (("v2", 1),):
                 L.call("irx_set_option", b"attn_v2", v2)
                 ms = timeit(lambda: O.attention(q, k, v, 8), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
+            if args.ref:   # torch SDPA (the ROCm flash / CK path) on the same data
+                hd = C // 8
+                qh, kh, vh = (t.view(B, -1, 8, hd).transpose(1, 2) for t in (q, k, v))
+                ms = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qh, kh, vh), args.iters)
+                res.append(f"sdpa {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             L.call("irx_set_option", b"attn_v2", 1)
             print(f"{lab:24s} " + " | ".join(res), flush=True)
 
