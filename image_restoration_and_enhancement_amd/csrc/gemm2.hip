@@ -423,6 +423,7 @@ void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
     IRX_LAUNCH_CHECK();
   }
   if (sp.splits > 1) {
+    ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::splitk_reduce_kernel") : std::string(), 0.0, s);
     const long n = (long)a.M * (a.N / 8);
     dim3 g2((unsigned)((n + 255) / 256), a.batch);
     if (a.out_f32) splitk_reduce_kernel<true><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits, sp.Mp, sp.Np);

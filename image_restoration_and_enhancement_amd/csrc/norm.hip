@@ -2,12 +2,13 @@
 //
 // GroupNorm (ResnetBlock2D norm1/norm2, Transformer2D norm, conv_norm_out, VAE attention norm):
 // two HBM-bound passes.  Pass 1 streams pixel chunks with 16-byte vector loads and accumulates
-// per-channel sum / sum of squares in fp64 (no E[x^2]-E[x]^2 cancellation at 40k-element groups),
-// folds them into per-group partials via LDS atomics.  Pass 2 finalises mean/rstd per (image,
-// group) from the partials, folds gamma/beta into one per-channel scale/shift, and writes
+// shifted per-channel sums in fp32, merged as sum / sum of squares in fp64 (no E[x^2]-E[x]^2
+// cancellation at 40k-element groups) into per-(image, chunk, group) partials; a small finalize
+// kernel folds them into mean/rstd.  Pass 2 folds gamma/beta into one per-channel scale/shift, and writes
 // y = x*a + b (optionally SiLU) with 16-byte vector stores.  Up-block inputs are a channel
 // concat of two tensors; groups may straddle the seam, so both passes read the two sources.
 #include "ops.h"
+#include "profile.h"
 
 namespace irx {
 namespace {
@@ -16,6 +17,24 @@ constexpr int kMaxChunks = 256;   // stats blocks per image (pixels per chunk gr
 
 int n_chunks(int HW) { return std::min((HW + 63) / 64, kMaxChunks); }
 int chunk_pix(int HW) { const int n = n_chunks(HW); return (HW + n - 1) / n; }
+
+// v3 stats: channel slabs (a power of two dividing G, <= 256 16-byte vectors each, >= 2 pixel rows per
+// block when C allows); 0 if G is not a power of two <= 64 (the v1 path runs)
+int gn_slabs(int C, int vec, int G) {
+  if (G <= 0 || G > 64 || (G & (G - 1))) return 0;
+  const int nv = C / vec;
+  for (int s = 1; s <= G; s *= 2)
+    if (nv % s == 0 && (C / s) % (C / G) == 0 && nv / s <= 128) return s;
+  for (int s = 1; s <= G; s *= 2)
+    if (nv % s == 0 && (C / s) % (C / G) == 0 && nv / s <= 256) return s;
+  return 0;
+}
+// pixel chunks per (image, slab): ~2048 blocks in all, >= 4 pixels per thread, <= kMaxChunks
+int gn_chunks3(int N, int HW, int slabs, int rows) {
+  const int want = (2048 + N * slabs - 1) / (N * slabs);
+  const int most = std::max(1, HW / (4 * rows));
+  return std::max(1, std::min(std::min(want, most), kMaxChunks));
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x0, const T* __restrict__ x1,
@@ -78,113 +97,103 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* __restrict__ x0,
   }
 }
 
-__device__ unsigned g_gn_arrivals[4096];   // per-image arrival counters of gn_stats2 (self-resetting)
-
-// GroupNorm statistics without LDS atomics, finalised in-kernel.  Pass 1: thread (16-byte channel vector,
-// pixel row r) accumulates shifted fp32 sums over its pixels and parks (shift, sum, sum of squares) per
-// channel in LDS.  Pass 2: one thread per group expands and merges them in fp64 and writes the chunk
-// partial.  The last chunk block of each image to arrive (agent-scope release/acquire around an arrival
-// counter) folds the image's partials into (mean, rstd) — no separate finalize launch.
+// GroupNorm statistics, v3: grid (pixel chunk, image, channel slab) sized to >= ~2048 blocks whatever the
+// resolution (the 8x8 / 16x16 UNet levels have too few pixels to fill the chip with pixel chunks alone).
+// Thread = one 16-byte channel vector x a pixel stride; 4 pixel loads in flight per thread; shifted fp32
+// sums per channel, expanded to raw fp64 (sum, sum of squares) in LDS; 8 threads per group fold the
+// block's channels/rows into one (sum, sum of squares) partial per (image, chunk, group);
+// gn_finalize3_kernel folds the partials into (mean, rstd).
 template <typename T>
-__global__ __launch_bounds__(256) void gn_stats2_kernel(const T* __restrict__ x0, const T* __restrict__ x1, int C0,
-                                                        int C1, int HW, int G, int cpix, double* part, float cnt_all,
-                                                        float eps, float2* __restrict__ mr) {
+__global__ __launch_bounds__(256) void gn_stats3_kernel(const T* __restrict__ x0, const T* __restrict__ x1, int C0,
+                                                        int C1, int HW, int G, int ppc, double* part) {
   constexpr int VEC = 16 / (int)sizeof(T);
-  extern __shared__ float tri[];               // [3][rows][C]: shift, sum, sum of squares
-  __shared__ double red[2][256];
-  __shared__ int last;
-  const int C = C0 + C1;
-  const int nv = C / VEC;
-  const int cg = C / G;
-  const int n = blockIdx.y, chunk = blockIdx.x, nch = gridDim.x;
-  const int p0 = chunk * cpix, p1 = min(HW, p0 + cpix);
-  const int rows = nv >= 256 ? 1 : 256 / nv;
-  const int r = threadIdx.x / (nv >= 256 ? 256 : nv);
-  float* X0 = tri;
-  float* S = tri + rows * C;
-  float* Q = tri + 2 * rows * C;
-  for (int vb = 0; vb < nv; vb += 256) {
-    const int v = vb + (nv >= 256 ? threadIdx.x : threadIdx.x % nv);
-    if (v >= nv || r >= rows) continue;
-    const int c = v * VEC;
-    const T* src = c < C0 ? x0 + c : x1 + (c - C0);
-    const int ld = c < C0 ? C0 : C1;
+  __shared__ double Sl[256 * VEC], Ql[256 * VEC];
+  const int C = C0 + C1, slabs = gridDim.z, Cs = C / slabs, nvs = Cs / VEC;
+  const int rows = 256 / nvs;
+  const int n = blockIdx.y, chunk = blockIdx.x, slab = blockIdx.z, nch = gridDim.x;
+  const int t = threadIdx.x, v = t % nvs, r = t / nvs;
+  const int p0 = chunk * ppc, p1 = min(HW, p0 + ppc);
+  if (r < rows) {
+    const int c = slab * Cs + v * VEC;
+    const T* src = c < C0 ? x0 + (long)n * HW * C0 + c : x1 + (long)n * HW * C1 + (c - C0);
+    const long ld = c < C0 ? C0 : C1;
     float s[VEC], q[VEC], xs[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) { s[e] = 0.f; q[e] = 0.f; xs[e] = 0.f; }
-    if (p0 + r < p1) Vec16<T>::unpack(*(const uint4*)(src + ((long)n * HW + p0 + r) * ld), xs);
-    for (int p = p0 + r; p < p1; p += rows) {
+    int p = p0 + r, cnt = 0;
+    if (p < p1) Vec16<T>::unpack(*(const uint4*)(src + p * ld), xs);
+    auto acc = [&](const uint4& u) {
       float f[VEC];
-      Vec16<T>::unpack(*(const uint4*)(src + ((long)n * HW + p) * ld), f);
+      Vec16<T>::unpack(u, f);
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
         const float dv = f[e] - xs[e];
         s[e] += dv;
         q[e] = fmaf(dv, dv, q[e]);
       }
+    };
+    for (; p + 3 * rows < p1; p += 4 * rows) {
+      const uint4 u0 = *(const uint4*)(src + p * ld);
+      const uint4 u1 = *(const uint4*)(src + (p + rows) * ld);
+      const uint4 u2 = *(const uint4*)(src + (p + 2 * rows) * ld);
+      const uint4 u3 = *(const uint4*)(src + (p + 3 * rows) * ld);
+      acc(u0); acc(u1); acc(u2); acc(u3);
+      cnt += 4;
     }
+    for (; p < p1; p += rows, ++cnt) acc(*(const uint4*)(src + p * ld));
 #pragma unroll
     for (int e = 0; e < VEC; ++e) {
-      X0[r * C + c + e] = xs[e];
-      S[r * C + c + e] = s[e];
-      Q[r * C + c + e] = q[e];
+      const double x = xs[e], sd = s[e];
+      Sl[t * VEC + e] = cnt * x + sd;
+      Ql[t * VEC + e] = cnt * x * x + 2.0 * x * sd + (double)q[e];
     }
   }
   __syncthreads();
-  if (threadIdx.x < G) {
-    const int g = threadIdx.x;
-    double sd = 0.0, qd = 0.0;
-    for (int rr = 0; rr < rows; ++rr) {
-      const int first = p0 + rr;
-      const double cnt = first < p1 ? (double)((p1 - first + rows - 1) / rows) : 0.0;
-      for (int c = g * cg; c < (g + 1) * cg; ++c) {
-        const double xv = X0[rr * C + c], sv = S[rr * C + c];
-        sd += cnt * xv + sv;
-        qd += cnt * xv * xv + 2.0 * xv * sv + (double)Q[rr * C + c];
-      }
-    }
-    double* o = part + (((long)n * nch + chunk) * G + g) * 2;
-    o[0] = sd;
-    o[1] = qd;
-  }
-  // ---- publish this chunk; the image's last arriving block finalises
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(&g_gn_arrivals[n], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == (unsigned)(nch - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  // threads t = g + G*j sum chunks j, j + 256/G, ...
-  const int per = 256 / G;
-  const int g = threadIdx.x % G, j = threadIdx.x / G;
-  double sd = 0.0, qd = 0.0;
-  if (j < per)
-    for (int ch = j; ch < nch; ch += per) {
-      const double* o = part + (((long)n * nch + ch) * G + g) * 2;
-      sd += o[0];
-      qd += o[1];
-    }
-  red[0][threadIdx.x] = sd;
-  red[1][threadIdx.x] = qd;
-  __syncthreads();
-  if (threadIdx.x < G) {
+  // fold rows x channels of each group (8 threads per group; G / slabs <= 32 groups in this slab)
+  const int Gs = G / slabs, cg = C / G;
+  {
+    const int gl = t >> 3, sub = t & 7;
     double a = 0.0, b = 0.0;
-    for (int jj = 0; jj < per; ++jj) { a += red[0][threadIdx.x + G * jj]; b += red[1][threadIdx.x + G * jj]; }
-    const double cnt = (double)cnt_all;
+    if (gl < Gs)
+      for (int i = sub; i < rows * cg; i += 8) {
+        const int rr = i / cg, ch = gl * cg + (i - rr * cg);
+        a += Sl[rr * Cs + ch];
+        b += Ql[rr * Cs + ch];
+      }
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
+    if (gl < Gs && sub == 0)
+      *(double2*)(part + (((long)n * nch + chunk) * G + slab * Gs + gl) * 2) = make_double2(a, b);
+  }
+}
+
+// per (image, group): fold the (chunk, slab) partials of gn_stats3 into (mean, rstd); 256 threads per
+// image, 256/G threads per group with 8 loads in flight each, shuffle-combined.  (A separate launch: an
+// in-kernel last-arriver finalize serialises ~2048 same-address arrival atomics, ~20 us at batch 16.)
+__global__ __launch_bounds__(256) void gn_finalize3_kernel(const double* __restrict__ part, int nch, int G,
+                                                           double cnt, float eps, float2* __restrict__ mr) {
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int per = 256 / G;                 // power of two (host check)
+  const int g = t / per, sub = t % per;
+  double a = 0.0, b = 0.0;
+  for (int base = sub; base < nch; base += 8 * per) {
+    double2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int ch = min(base + u * per, nch - 1);
+      v[u] = *(const double2*)(part + (((long)n * nch + ch) * G + g) * 2);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (base + u * per < nch) { a += v[u].x; b += v[u].y; }
+  }
+  for (int o = per / 2; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
+  if (sub == 0) {
     const double mean = a / cnt;
     double var = b / cnt - mean * mean;
     if (var < 0.0) var = 0.0;
-    mr[n * G + threadIdx.x] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+    mr[n * G + g] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
   }
-  if (threadIdx.x == 0) g_gn_arrivals[n] = 0u;   // ready for the next call on this stream
 }
 
 // per (image, group): fold the chunk partials into (mean, rstd) once
@@ -311,14 +320,20 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
           const float* beta, int silu, void* out, void* ws, hipStream_t s) {
   const int nch = n_chunks(HW);
   double* part = (double*)ws;
-  float2* mr = (float2*)(part + (size_t)N * nch * G * 2);
+  float2* mr = (float2*)(part + (size_t)N * kMaxChunks * G * 2);
   const int C = C0 + C1;
   const int VEC = 16 / (int)sizeof(T);
   const int nvv = C / VEC;
   const int rws = nvv >= 256 ? 1 : 256 / nvv;
-  if (g_gn_v2 && N <= 4096 && 3 * rws * C * sizeof(float) <= 60 * 1024) {   // default dynamic-LDS limit
-    gn_stats2_kernel<T><<<dim3(nch, N), 256, 3 * rws * C * sizeof(float), s>>>(
-        (const T*)x0, (const T*)x1, C0, C1, HW, G, chunk_pix(HW), part, (float)HW * (C / G), eps, mr);
+  const int slabs = gn_slabs(C, VEC, G);
+  if (g_gn_v2 && N <= 4096 && slabs > 0) {
+    ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_stats3_kernel") : std::string(), 0.0, s);
+    const int rows3 = 256 / (C / slabs / VEC);
+    const int nch3 = gn_chunks3(N, HW, slabs, rows3);
+    gn_stats3_kernel<T><<<dim3(nch3, N, slabs), 256, 0, s>>>(
+        (const T*)x0, (const T*)x1, C0, C1, HW, G, (HW + nch3 - 1) / nch3, part);
+    IRX_LAUNCH_CHECK();
+    gn_finalize3_kernel<<<N, 256, 0, s>>>(part, nch3, G, (double)HW * (C / G), eps, mr);
     IRX_LAUNCH_CHECK();
   } else {
     gn_stats_kernel<T><<<dim3(nch, N), 256, 0, s>>>((const T*)x0, (const T*)x1, C0, C1, HW, G, chunk_pix(HW),
@@ -330,7 +345,10 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
   // ~16 pixels per thread per block, one fixed channel chunk per thread
   const int nv = C / VEC;
   const int rows = nv >= 256 ? 1 : 256 / nv;
-  const int ppb = rows * 16;
+  // pixels per thread: up to 16, fewer when the tensor is small, so the grid still has ~2048 blocks
+  const int ppt = std::max(1, std::min(16, (int)((long)N * HW / ((long)rows * 2048))));
+  const int ppb = rows * ppt;
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_apply_kernel") : std::string(), 0.0, s);
   gn_apply_kernel<T><<<dim3((HW + ppb - 1) / ppb, N), 256, 2 * C * sizeof(float), s>>>(
       (const T*)x0, (const T*)x1, C0, C1, HW, G, mr, gamma, beta, silu, (T*)out, ppb);
   IRX_LAUNCH_CHECK();
@@ -342,6 +360,7 @@ void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamm
   const int VEC = 16 / (int)sizeof(T);
   const int nv = C / VEC;
   dim3 grid((rows + 3) / 4), block(256);
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::ln_kernel") : std::string(), 0.0, s);
   if (nv <= 64) ln_kernel<T, 1><<<grid, block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
   else if (nv <= 128) ln_kernel<T, 2><<<grid, block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
   else if (nv <= 256) ln_kernel<T, 4><<<grid, block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
@@ -352,10 +371,11 @@ void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamm
 
 }  // namespace
 
-bool g_gn_v2 = true;   // irx_set_option("gn_v2", 0): LDS-atomic stats + separate finalize (A/B)
+bool g_gn_v2 = true;   // irx_set_option("gn_v2", 0): v1 LDS-atomic stats + separate finalize (A/B)
 
 size_t gn_ws_bytes(int N, int HW, int G) {
-  return (size_t)N * n_chunks(HW) * G * 2 * sizeof(double) + (size_t)N * G * sizeof(float2);
+  (void)HW;   // partials for up to kMaxChunks chunks per image (v1 and v3 layouts)
+  return (size_t)N * kMaxChunks * G * 2 * sizeof(double) + (size_t)N * G * sizeof(float2);
 }
 
 void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,

@@ -138,8 +138,7 @@ def test_gemm_batched(device, dt):
 @pytest.mark.parametrize("C0,C1,H,W,silu,eps", [(320, 0, 16, 16, True, 1e-5), (1280, 640, 8, 8, True, 1e-5),
                                                 (128, 0, 33, 20, False, 1e-6), (640, 0, 7, 5, False, 1e-6),
                                                 (2560, 0, 4, 4, True, 1e-5)])
-def test_group_norm(device, dt, C0, C1, H, W, silu, eps):
-    N = 2
+def test_group_norm(device, dt, C0, C1, H, W, silu, eps, N=2):
     x0 = _r(N, C0, H, W, seed=30) * 3 + 1.5        # offset mean: exercises the variance path
     x1 = _r(N, C1, H, W, seed=31) if C1 else None
     g, b = 1 + 0.1 * _r(C0 + C1, seed=32), 0.1 * _r(C0 + C1, seed=33)
@@ -149,6 +148,13 @@ def test_group_norm(device, dt, C0, C1, H, W, silu, eps):
     ref = F.group_norm(xin, 32, g, b, eps)
     ref = (F.silu(ref) if silu else ref).permute(0, 2, 3, 1)
     assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("N,C0,C1,H,W", [(16, 2560, 0, 8, 8), (16, 1280, 1280, 8, 8), (16, 1280, 640, 16, 16),
+                                         (16, 320, 0, 64, 64), (3, 128, 0, 96, 80), (16, 960, 0, 5, 3)])
+def test_group_norm_unet_shapes(device, N, C0, C1, H, W):
+    """Batch-16 UNet level shapes: channel slabs (C >= 2048), multi-chunk images, tiny images."""
+    test_group_norm(device, torch.bfloat16, C0, C1, H, W, True, 1e-5, N=N)
 
 
 @pytest.mark.parametrize("dt", DTS)
