@@ -62,6 +62,9 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gemm_deep") g_gemm_deep = value;
   else if (n == "gemm_dbg") g_gemm_dbg = value;
   else if (n == "gn_v2") g_gn_v2 = value != 0;
+  else if (n == "splitk_inkernel") g_splitk_inkernel = value != 0;
+  else if (n == "tile_256x320") g_tile_256x320 = value != 0;
+  else if (n == "gemm_force") g_gemm_force = value;
   else if (n == "gemm_small") g_gemm_small = value != 0;
   else if (n == "attn_d40") g_attn_d40 = value;
   else if (n == "gemm_small_kmax") g_gemm_small_kmax = value;

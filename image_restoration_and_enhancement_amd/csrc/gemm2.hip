@@ -16,6 +16,7 @@
 //   * XCD-aware block -> tile mapping (tiles sharing an A panel on one XCD's L2).
 // Requirements (else the 4-wave kernel in gemm.hip runs): bf16, K % 64 == 0, conv channel
 // counts % 64 == 0 (a 64-deep K step never straddles a tap or the concat seam).
+#include <cmath>
 #include <mutex>
 
 #include "ops.h"
@@ -29,7 +30,12 @@ namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+typedef __attribute__((address_space(1))) unsigned gu32;
+constexpr int kSplitCounters = 1 << 16;
+__device__ unsigned g_splitk_cnt[kSplitCounters];   // per-(batch, tile) split arrival tickets (self-resetting)
+
 struct Split {
+  bool inkernel = false;   // last arriving split reduces (else splitk_reduce_kernel)
   int splits = 1;      // K splits (gridDim.y = batch * splits)
   int per = 0;         // K steps per split
   float* ws = nullptr; // fp32 partials [batch*splits][Mp][Np] (M, N rounded up to the tile: unchecked stores)
@@ -253,17 +259,63 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     if (t == 12345.678f) ((float*)a.C)[0] = t;
     return;
   }
-  // ---- split-K: raw fp32 partial tile, epilogue applied by splitk_reduce_kernel
+  // ---- split-K: raw fp32 partial tile.  In-kernel mode: partials stored write-through (sc1), one relaxed
+  //      agent-scope ticket per block; the tile's last arriving split adds the others' partials (sc1
+  //      loads) into its accumulators and runs the normal epilogue (no release / acquire fences: they
+  //      would write back / invalidate whole caches).  Otherwise splitk_reduce_kernel finishes.
   if (sp.splits > 1) {
-    float* P = sp.ws + (long)blockIdx.y * sp.Mp * sp.Np + (long)(m0 + wm * TM * 16 + fgrp * 4) * sp.Np + n0 +
-               wn * TN * 16 + frow;
+    const long poff = (long)(m0 + wm * TM * 16 + fgrp * 4) * sp.Np + n0 + wn * TN * 16 + frow;
+    float* P = sp.ws + (long)blockIdx.y * sp.Mp * sp.Np + poff;
+    if (!sp.inkernel) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) P[(long)(i * 16 + r) * sp.Np + j * 16] = acc[i][j][r];
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) P[(long)(i * 16 + r) * sp.Np + j * 16] = acc[i][j][r];
-    return;
+        for (int r = 0; r < 4; ++r)
+          __hip_atomic_store((gu32*)(P + (long)(i * 16 + r) * sp.Np + j * 16), __float_as_uint(acc[i][j][r]),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+    __syncthreads();
+    int* flag = (int*)smem;                             // (one LDS array: no second __shared__ object)
+    const int cidx = z * tiles_m * tiles_n + bid;
+    if (tid == 0) {
+      const unsigned prev = __hip_atomic_fetch_add((gu32*)&g_splitk_cnt[cidx], 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+      *flag = prev == (unsigned)(sp.splits - 1);
+    }
+    __syncthreads();
+    const bool is_last = *flag != 0;
+    __syncthreads();                                    // flag read by every wave before smem is reused
+    if (!is_last) return;
+    for (int s2 = 0; s2 < sp.splits; ++s2) {
+      if (s2 == ks) continue;
+      const float* Q = sp.ws + (long)(z * sp.splits + s2) * sp.Mp * sp.Np + poff;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        uint32_t v[TN][4];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            v[j][r] = __hip_atomic_load((gu32*)(Q + (long)(i * 16 + r) * sp.Np + j * 16), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += __uint_as_float(v[j][r]);
+      }
+    }
+    if (tid == 0)   // ready for the next launch (the kernel boundary orders it)
+      __hip_atomic_store((gu32*)&g_splitk_cnt[cidx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
   // ---- epilogue (D[row = 4g + r][col = lane & 15] per 16x16 tile)
@@ -422,7 +474,7 @@ void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
     }
     IRX_LAUNCH_CHECK();
   }
-  if (sp.splits > 1) {
+  if (sp.splits > 1 && !sp.inkernel) {
     ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::splitk_reduce_kernel") : std::string(), 0.0, s);
     const long n = (long)a.M * (a.N / 8);
     dim3 g2((unsigned)((n + 255) / 256), a.batch);
@@ -453,25 +505,45 @@ Choice choose(const GemmArgs& a) {
       return best;
     }
   }
+  if (g_gemm_force > 0 && g_gemm_deep == 0) {   // tuning sweeps: BM*100000 + BN*100 + splits
+    const int BM = g_gemm_force / 100000, BN = (g_gemm_force / 100) % 1000, sp = g_gemm_force % 100;
+    const bool ok = (BM == 256 || BM == 128) && (BN == 320 || BN == 256 || BN == 128) && a.N % BN == 0 &&
+                    sp >= 1 && (sp == 1 || !((a.out_f32 && a.batch > 1) || a.geglu)) && (!a.geglu || BN % 128 == 0) &&
+                    !(BM == 256 && BN == 128);   // (256x128 is a 4x2-wave shape: not forced)
+    if (ok) {
+      best.BM = BM; best.BN = BN; best.splits = sp; best.per = (nk + sp - 1) / sp;
+      if ((long)(sp - 1) * best.per < nk) return best;
+    }
+    best = Choice();
+  }
   double best_score = -1.0;
-  const int cands[6][2] = {{256, 256}, {128, 320}, {256, 128}, {128, 256}, {128, 128}, {256, 160}};
+  const int cands[7][2] = {{256, 320}, {256, 256}, {128, 320}, {256, 128}, {128, 256}, {128, 128}, {256, 160}};
   for (auto& c : cands) {
     const int BM = c[0], BN = c[1];
     if (BN == 160 && g_gemm_deep != 2) continue;
+    if (BN == 320 && BM == 256 && (g_gemm_deep != 0 || !g_tile_256x320)) continue;
     if (a.N % BN != 0) continue;
     if (a.geglu && BN % 128 != 0) continue;      // tiles must hold whole (value, gate) block pairs
     const long tiles = (long)((a.M + BM - 1) / BM) * (a.N / BN) * a.batch;
-    const double intensity = (double)BM * BN / (BM + BN) / 128.0;   // 256x256 == 1
+    // per-tile efficiency at full occupancy, calibrated on the batch-16 UNet / batch-8 VAE shapes
+    // (scripts/gemm_sweep.py): the load path (L2 -> LDS-DMA) bounds the small tiles, 128x128 keeps two
+    // blocks per CU resident (its prologue / epilogue overlap the other block's loop), 256x128 (4x2 waves)
+    // loses to it everywhere measured
+    const double eff = BM == 256 ? (BN >= 256 ? 1.0 : BN == 160 ? 0.9 : 0.65)
+                                 : (BN == 320 ? 0.97 : BN == 256 ? 0.75 : 0.78);
+    const int resident = (BM == 128 && BN == 128 && g_gemm_deep == 0) ? 2 : 1;
+    const long cap = (long)kCUs * resident;
     for (int splits = 1; splits <= 8; splits *= 2) {
       if (splits > 1 && ((a.out_f32 && a.batch > 1) || a.geglu)) break;
       const int per = (nk + splits - 1) / splits;
       if (per * step_k() < 512 && splits > 1) break;    // keep >= 512 of K per split
       if ((long)(splits - 1) * per >= nk) break;        // no empty split
       const long blocks = tiles * splits;
-      const double util = (double)blocks / ((double)((blocks + kCUs - 1) / kCUs) * kCUs);
-      // split-K pays an fp32 partial write + read of the output per split
-      const double cost_split = splits > 1 ? 1.0 + 0.06 * splits : 1.0;
-      const double score = util * intensity / cost_split;
+      const double util = (double)blocks / ((double)((blocks + cap - 1) / cap) * cap);
+      // split-K pays an fp32 partial write + read per split and a reduction tail, relatively more when
+      // each split is short
+      const double cost_split = splits > 1 ? (1.0 + 0.35 * std::log2((double)splits)) * (per < 16 ? 1.6 : 1.0) : 1.0;
+      const double score = util * eff / cost_split;
       if (score > best_score + 1e-9) {
         best_score = score;
         best.BM = BM; best.BN = BN; best.splits = splits; best.per = per;
@@ -522,6 +594,9 @@ int g_gemm_deep = 0;   // irx_set_option("gemm_deep", m): 0 two-stage BK 64, 1 B
 int g_gemm_dbg = 0;
 bool g_gemm_small = false;   // irx_set_option("gemm_small", 1): 4-wave 128x160 / 128x128 tiles for K <= kmax
 int g_gemm_small_kmax = 1280;
+bool g_splitk_inkernel = true;   // irx_set_option("splitk_inkernel", 0): separate split-K reduce kernel (A/B)
+bool g_tile_256x320 = true;      // irx_set_option("tile_256x320", 0): no 256x320 tiles (A/B)
+int g_gemm_force = 0;            // irx_set_option("gemm_force", BM*100000 + BN*100 + splits): tuning sweeps
 
 bool gemm_geglu_fusable(const GemmArgs& a) {
   if (!g_large_tiles || !a.geglu || !eligible(a) || !vec_ok(a)) return false;
@@ -555,6 +630,9 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     sp.Np = (a.N + c.BN - 1) / c.BN * c.BN;
     const size_t need = (size_t)c.splits * a.batch * sp.Mp * sp.Np * sizeof(float);
     sp.ws = (a.splitk_ws && a.splitk_ws_bytes >= need) ? (float*)a.splitk_ws : internal_ws(need);
+    const long tiles = (long)((a.M + c.BM - 1) / c.BM) * ((a.N + c.BN - 1) / c.BN) * a.batch;
+    // in-kernel reduction wins at 2 splits; with more, the serial last-arriver tail loses to the reduce kernel
+    sp.inkernel = g_splitk_inkernel && c.splits == 2 && tiles <= kSplitCounters;
   } else {
     sp.per = a.K / step_k();
   }
@@ -582,6 +660,7 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     }
   } else {
     switch (c.BM * 1000 + c.BN) {
+      case 256320: launch2<256, 320, 2, 4, 64, 2>(b, sp, s); break;
       case 256256: launch2<256, 256, 2, 4, 64, 2>(b, sp, s); break;
       case 128320: launch2<128, 320, 2, 4, 64, 2>(b, sp, s); break;
       case 256128: launch2<256, 128, 4, 2, 64, 2>(b, sp, s); break;

@@ -56,6 +56,9 @@ extern int g_gemm_small_kmax;
 // GroupNorm over NHWC (optionally a channel concat of two sources). Writes the normalised (and
 // optionally SiLU'd) result as one contiguous C0+C1 channel tensor.  `ws` needs gn_ws_bytes().
 size_t gn_ws_bytes(int N, int HW, int G);
+extern bool g_splitk_inkernel;
+extern bool g_tile_256x320;
+extern int g_gemm_force;
 extern bool g_gn_v2;       // GroupNorm stats v3 (slabbed grid + finalize kernel); 0 = v1 (A/B)
 void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
                 const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s);

@@ -70,8 +70,14 @@ def main():
     L.load()
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
-    allv = {"s2": (1, 0, 0), "ring64": (1, 2, 0), "small": (1, 0, 1), "4wave": (0, 0, 0)}
+    base = {"large_tiles": 1, "gemm_deep": 0, "gemm_small": 0, "tile_256x320": 1, "splitk_inkernel": 1}
+    allv = {"s2": {}, "ring64": {"gemm_deep": 2}, "small": {"gemm_small": 1}, "4wave": {"large_tiles": 0},
+            "no320": {"tile_256x320": 0}, "redk": {"splitk_inkernel": 0}, "no320redk": {"tile_256x320": 0, "splitk_inkernel": 0}}
     variants = [(v, allv[v]) for v in args.variants.split(",")]
+
+    def setv(opts):
+        for k, v in {**base, **opts}.items():
+            L.call("irx_set_option", k.encode(), v)
     if args.only in ("", "conv"):
         for lab, N, H, W, C0, C1, Co, k, s, up in CONVS:
             x0 = torch.randn(N, H, W, C0, device=dev, generator=g).to(dt)
@@ -81,10 +87,8 @@ def main():
             Ho, Wo = up if up else (H, W)
             flops = 2.0 * N * Ho * Wo * Co * (C0 + C1) * k * k
             res = []
-            for vn, (lt, dp, sm) in variants:
-                L.call("irx_set_option", b"large_tiles", lt)
-                L.call("irx_set_option", b"gemm_deep", dp)
-                L.call("irx_set_option", b"gemm_small", sm)
+            for vn, opts in variants:
+                setv(opts)
                 ms = timeit(lambda: O.conv2d(x0, w, b, x1=x1, up_hw=up), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             if args.ref:   # MIOpen (torch) channels-last bf16 conv on the same data: a known-good reference
@@ -102,10 +106,8 @@ def main():
             Bw = (torch.randn(N, K, device=dev, generator=g) / math.sqrt(K)).to(dt)
             flops = 2.0 * M * N * K
             res = []
-            for vn, (lt, dp, sm) in variants:
-                L.call("irx_set_option", b"large_tiles", lt)
-                L.call("irx_set_option", b"gemm_deep", dp)
-                L.call("irx_set_option", b"gemm_small", sm)
+            for vn, opts in variants:
+                setv(opts)
                 ms = timeit(lambda: O.gemm(A, Bw), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             if args.ref:   # hipBLASLt (torch.matmul) on the same data: a known-good reference
@@ -113,9 +115,7 @@ def main():
                 ms = timeit(lambda: torch.matmul(A, Bt), args.iters)
                 res.append(f"hipblaslt {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             print(f"{lab:24s} " + " | ".join(res), flush=True)
-    L.call("irx_set_option", b"large_tiles", 1)
-    L.call("irx_set_option", b"gemm_deep", 0)
-    L.call("irx_set_option", b"gemm_small", 0)
+    setv({})
     if args.only in ("", "attn"):
         for lab, B, Lq, Lk, C in ATTNS:
             q = torch.randn(B, Lq, C, device=dev, generator=g).to(dt)

@@ -295,3 +295,23 @@ def test_gemm_large_batched(device, tiles):
     got = O.gemm(_dev(A, dt, device), _dev(Bw, dt, device), batch=b, out_f32=True)
     ref = torch.bmm(_q(A, dt), _q(Bw, dt).transpose(1, 2))
     assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("inkernel", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(4096, 1280, 1280), (1024, 1280, 2560), (4096, 640, 5120)])
+def test_gemm_splitk_modes(device, inkernel, M, N, K):
+    """Split-K shapes (few output tiles, long K) with the in-kernel last-arriver reduction and with the
+    separate reduce kernel; bias + residual run in whichever epilogue finishes the tile."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    dt = torch.bfloat16
+    A = _r(M, K, seed=90)
+    Bw = _r(N, K, seed=91, scale=1 / math.sqrt(K))
+    bias, R = _r(N, seed=92), _r(M, N, seed=93)
+    L.call("irx_set_option", b"splitk_inkernel", inkernel)
+    try:
+        for _ in range(2):   # second call: the arrival tickets must have been reset
+            got = O.gemm(_dev(A, dt, device), _dev(Bw, dt, device), bias=bias.to(device), residual=_dev(R, dt, device))
+            ref = _q(A, dt) @ _q(Bw, dt).T + bias + _q(R, dt)
+            assert O.rel_err(got, ref) < TOL[dt]
+    finally:
+        L.call("irx_set_option", b"splitk_inkernel", 1)
