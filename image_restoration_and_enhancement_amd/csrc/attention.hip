@@ -289,8 +289,8 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
 // KT keys per LDS tile (128 at d <= 80, 64 at d = 160 to bound registers); 4 waves x 32 queries.
 // ONES: the head dim leaves a zero pad column in V (d < DV); it is set to 1 so the PV MFMAs also produce
 // the softmax row sums (O^T row d = sum_k P[q][k]) and the per-score VALU add disappears.
-template <int DQ, int DV, int KT, bool ONES>
-__global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
+template <int DQ, int DV, int KT, bool ONES, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
   constexpr int SK = DQ + 8;                                     // 16 rows x b128 reads conflict-free
   constexpr int SV = ((DV * 2 / 32) % 2 == 1) ? DV : DV + 16;    // 8 rows x 32 B tr reads conflict-free
   // QK^T contracts over DQ = 32 * NDC (head dim zero-padded).  (A 16x16x16 MFMA for a d % 32 == 8..16 tail was
@@ -484,7 +484,10 @@ __global__ __launch_bounds__(256, 2) void attn2_kernel(AttnArgs a) {
 
 void launch_bf16(const AttnArgs& a, hipStream_t s) {
   dim3 grid((a.Lq + kQB - 1) / kQB, a.H, a.B), block(256);
-  const char* inst = a.d == 40 ? (g_attn_d40 == 1 ? "64, 48, 128, false" : "64, 48, 128, true")
+  const char* inst = a.d == 40 ? (g_attn_d40 == 1   ? "64, 48, 128, false"
+                                  : g_attn_d40 == 2 ? "64, 48, 64, true, 3"
+                                  : g_attn_d40 == 3 ? "64, 48, 64, true, 4"
+                                                    : "64, 48, 128, true, 2")
                      : a.d == 64 ? "64, 64, 128, false"
                      : a.d == 80 ? "96, 80, 64, false" : "160, 160, 32, false";
   ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn2_kernel<") + inst + ">" : std::string(),
@@ -492,6 +495,8 @@ void launch_bf16(const AttnArgs& a, hipStream_t s) {
   switch (a.d) {
     case 40:
       if (g_attn_d40 == 1) attn2_kernel<64, 48, 128, false><<<grid, block, 0, s>>>(a);
+      else if (g_attn_d40 == 2) attn2_kernel<64, 48, 64, true, 3><<<grid, block, 0, s>>>(a);
+      else if (g_attn_d40 == 3) attn2_kernel<64, 48, 64, true, 4><<<grid, block, 0, s>>>(a);
       else attn2_kernel<64, 48, 128, true><<<grid, block, 0, s>>>(a);
       break;
     case 64: attn2_kernel<64, 64, 128, false><<<grid, block, 0, s>>>(a); break;
@@ -535,6 +540,7 @@ void attention(const AttnArgs& a, hipStream_t s) {
 }
 
 bool g_attn_v2 = true;
-int g_attn_d40 = 0;   // d = 40 variant (A/B): 0 ones-column row sums, 1 VALU row sums
+int g_attn_d40 = 2;   // d = 40 variant (A/B): 0 128-key tiles (ones-column row sums), 1 VALU row sums,
+                      // 2/3 64-key tiles at 3/4 blocks per CU (2, default: +8% self, +40% cross-attention; 3 spills)
 
 }  // namespace irx
