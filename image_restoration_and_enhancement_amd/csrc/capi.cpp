@@ -65,6 +65,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "splitk_inkernel") g_splitk_inkernel = value != 0;
   else if (n == "tile_256x320") g_tile_256x320 = value != 0;
   else if (n == "gemm_force") g_gemm_force = value;
+  else if (n == "conv_halo") g_conv_halo = value;
   else if (n == "gemm_small") g_gemm_small = value != 0;
   else if (n == "attn_d40") g_attn_d40 = value;
   else if (n == "gemm_small_kmax") g_gemm_small_kmax = value;

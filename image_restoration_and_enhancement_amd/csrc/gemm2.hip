@@ -66,7 +66,14 @@ __device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds_addr) {
 // BK: K depth of one LDS stage (64: 8 chunks of 16 B per row, 32: 4); S: stages in the ring.
 // S == 2 is the classic double buffer (drain + barrier per step); S > 2 keeps S-2 stages of LDS-DMA in
 // flight across each (raw) barrier, waiting with a counted vmcnt for exactly the stage about to be read.
-template <int BM, int BN, int WM, int WN, int BK, int S, bool CONV, bool OUTF32, bool RESIZE>
+// HALO (3x3 / stride 1 / pad 1 convs whose block tile is BM/W whole image rows): the A operand is not an
+// im2col gather per K step but the tile's (rows + 2) x W pixel halo of one BK-channel slab, DMA'd into
+// LDS once per slab and read by all 9 taps through shifted fragment addresses.  Per slab a block moves
+// one halo + 9 B panels instead of 9 A panels + 9 B panels (1.5x fewer L2 -> LDS bytes per MFMA at
+// 256x160 than the 256x320 im2col tile), with whole 128-B lines per request (BK 64).
+constexpr int kHaloWMax = 64;    // widest image row a halo tile takes (LDS: 2 x (BM + 2W) x 2BK B)
+
+template <int BM, int BN, int WM, int WN, int BK, int S, bool CONV, bool OUTF32, bool RESIZE, bool HALO = false>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kernel(GemmArgs a, Split sp) {
   constexpr int NW = WM * WN, NT = NW * 64;   // 8 waves (1 block/CU) or 4 waves (2 blocks/CU)
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
@@ -78,7 +85,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   constexpr int STAGE = ROWS * CPR;          // uint4 per stage
   constexpr int KSUB = BK / 32;              // 32-deep MFMA sub-steps per stage
   static_assert((NW == 8 || NW == 4) && ROWS % RPI == 0 && BM % 16 == 0 && (BK == 32 || BK == 64), "tile shape");
-  constexpr int SMEM = (S * STAGE > BM * BN / 8 ? S * STAGE : BM * BN / 8) + (NINST % NW ? 64 : 0);
+  static_assert(!HALO || (CONV && !RESIZE && S >= 2 && S <= 8 && NW == 8), "halo tiles: 3x3 conv");
+  constexpr int HB_U4 = (BM + 2 * kHaloWMax) * CPR;   // one halo slab buffer (uint4)
+  constexpr int RING = HALO ? 2 * HB_U4 + S * BN * CPR + CPR + 64 : S * STAGE;
+  constexpr int SMEM = (RING > BM * BN / 8 ? RING : BM * BN / 8) + (!HALO && NINST % NW ? 64 : 0);
+  static_assert(SMEM * 16 <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) uint4 smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -156,7 +167,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       rb[j] = ok ? sb + pix * cs : nullptr;
     }
   };
-  if constexpr (CONV) {
+  if constexpr (CONV && !HALO) {
     const int k = kt0 * BK;
     const int tap = k / Cin;
     kc = k - tap * Cin;
@@ -221,7 +232,117 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     }
   };
 
-  if constexpr (S == 2) {
+  if constexpr (HALO) {
+    // ---- halo main loop: K step kt = (slab c = kt / 9, tap t = kt % 9), a slab = BK channels; host
+    //      guarantees W = 2^lw in [16, kHaloWMax], BM % W == 0, H % (BM / W) == 0, C0 % BK == C1 % BK == 0,
+    //      one split (kt0 = 0).
+    //      B panels run through an S-stage ring (S-2 steps of DMA in flight across each barrier); slab
+    //      c+1's halo is issued at tap 0 of slab c into the other halo buffer.  Every wave issues the same
+    //      number of DMA pieces per step (surplus pieces land in a scratch KiB), so one counted vmcnt per
+    //      step covers both streams.
+    const int W = a.g.Win, H = a.g.Hin, lw = __builtin_ctz(W);
+    const int HW = H * W;
+    const int img = m0 / HW, y0 = (m0 - img * HW) >> lw;
+    const int nhi = (((BM >> lw) + 2) << lw) / RPI;   // halo wave-instructions (RPI pixel rows each)
+    const int hpw = (nhi + NW - 1) / NW;              // ... per wave
+    uint4* const Hb = smem;                           // [2][HB_U4]
+    uint4* const Bsm = smem + 2 * HB_U4;              // [S][BN * CPR]
+    uint4* const zrow = Bsm + S * BN * CPR;           // one zero pixel row: taps left / right of the image
+    uint4* const scratch = zrow + CPR;                // 1 KiB target of the surplus pieces
+    if (tid < CPR) zrow[tid] = uint4{0u, 0u, 0u, 0u};
+    // chunk slot XOR swz(row), conflict-free ds_read_b128 fragments for any row shift in {-1, 0, +1} (the
+    // kx taps), checked against the gfx950 lane groups: 128-B rows r & 7, 64-B rows 2 * bit2(r)
+    auto swz = [](int r) { return CPR == 8 ? (r & 7) : (((r >> 2) & 1) << 1); };
+    constexpr int NBI = BN / RPI, IPB = (NBI + NW - 1) / NW;
+    const uint16_t* bro[IPB];
+#pragma unroll
+    for (int j = 0; j < IPB; ++j) {
+      const int q = wave * IPB + j, r = RPI * q + lane / CPR;
+      bro[j] = (q < NBI && n0 + r < a.N) ? Bp + (long)(n0 + r) * a.ldb + (((lane % CPR) ^ swz(r)) * 8) : nullptr;
+    }
+    auto issueB = [&](int kt, int st) {
+      const int c = kt / 9, t = kt - 9 * c;
+      const int off = t * Cin + c * BK;
+#pragma unroll
+      for (int j = 0; j < IPB; ++j) {
+        const int q = wave * IPB + j;
+        uint4* dst = q < NBI ? Bsm + st * BN * CPR + q * 64 : scratch;
+        glds16_asm(bro[j] ? bro[j] + off : zp, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
+      }
+    };
+    auto issueH = [&](int c) {
+      const bool second = c * BK >= a.g.C0;
+      const uint16_t* sb = second ? (const uint16_t*)a.g.src1 : (const uint16_t*)a.g.src0;
+      const int cs = second ? a.g.C1 : a.g.C0;
+      const int ch = second ? c * BK - a.g.C0 : c * BK;
+#pragma unroll 1
+      for (int j = 0; j < hpw; ++j) {
+        const int q = wave * hpw + j;
+        const int p = RPI * q + lane / CPR;
+        const int y = y0 - 1 + (p >> lw), x = p & (W - 1);
+        const bool ok = q < nhi && y >= 0 && y < H;
+        const uint16_t* src = ok ? sb + ((long)(img * H + y) * W + x) * cs + ch + (((lane % CPR) ^ swz(p)) * 8) : zp;
+        uint4* dst = q < nhi ? Hb + (c & 1) * HB_U4 + q * 64 : scratch;
+        glds16_asm(src, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
+      }
+    };
+    const int nk = kt1;   // (kt0 == 0)
+    issueH(0);
+#pragma unroll
+    for (int p = 0; p < S - 1; ++p)
+      if (p < nk) issueB(p, p);
+    __syncthreads();      // zero row visible
+    int st = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int c = kt / 9, t = kt - 9 * c;
+      // younger than B(kt): B(kt+1 .. kt+S-2), and slab c+1's halo while it was issued after B(kt)
+      int allow = IPB * min(S - 2, nk - 1 - kt);
+      if (t >= 1 && t <= S - 1 && 9 * (c + 1) < nk) allow += hpw;
+      wait_vm(__builtin_amdgcn_readfirstlane(allow));
+      asm volatile("s_barrier" ::: "memory");   // everyone's pieces landed; everyone finished reading kt-1
+      if (kt + S - 1 < nk) issueB(kt + S - 1, st == 0 ? S - 1 : st - 1);
+      if (t == 0 && 9 * (c + 1) < nk) issueH(c + 1);
+      if (!(a.dbg & 2)) {
+        const int ky = t / 3, kx = t - 3 * ky;
+        const int shift = ky * W + kx - 1;
+        const uint4* Hs = Hb + (c & 1) * HB_U4;
+        const uint4* Bs = Bsm + st * BN * CPR;
+        // every sub-step's fragments are requested before the first MFMA: the LDS latency of sub-step
+        // s+1 hides under the MFMAs of sub-step s (one register set per sub-step)
+        uint4 af[KSUB][TM], bfr[KSUB][TN];
+#pragma unroll
+        for (int ss = 0; ss < KSUB; ++ss) {
+          const int ck = ss * 4 + fgrp;
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const int r = wm * TM * 16 + i * 16 + frow;
+            const int rx = r & (W - 1);
+            const int hp = r + shift;
+            const bool zero = (kx == 0 && rx == 0) || (kx == 2 && rx == W - 1);
+            af[ss][i] = zero ? zrow[ck] : Hs[hp * CPR + (ck ^ swz(hp))];
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int r = wn * TN * 16 + j * 16 + frow;
+            bfr[ss][j] = Bs[r * CPR + (ck ^ swz(r))];
+          }
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ss = 0; ss < KSUB; ++ss)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[ss][i]),
+                                                                  __builtin_bit_cast(bf16x8, bfr[ss][j]), acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      st = st + 1 == S ? 0 : st + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else if constexpr (S == 2) {
     if (kt0 < kt1) issue(kt0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -452,7 +573,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int S>
+template <int BM, int BN, int WM, int WN, int BK, int S, bool HALO = false>
 void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, a.batch * sp.splits), block(WM * WN * 64);
@@ -462,10 +583,12 @@ void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
     nm = "irx::(anonymous namespace)::gemm2_kernel<" + std::to_string(BM) + ", " + std::to_string(BN) + ", " +
          std::to_string(WM) + ", " + std::to_string(WN) + ", " + std::to_string(BK) + ", " + std::to_string(S) +
          ", " + (a.conv ? "true" : "false") + ", " + (a.out_f32 ? "true" : "false") + ", " +
-         (rs ? "true" : "false") + ">";
+         (rs ? "true" : "false") + ", " + (HALO ? "true" : "false") + ">";
   {
     ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
-    if (a.conv) {   // (fp32-output convs never take this path: see eligible())
+    if constexpr (HALO) {
+      gemm2_kernel<BM, BN, WM, WN, BK, S, true, false, false, true><<<grid, block, 0, s>>>(a, sp);
+    } else if (a.conv) {   // (fp32-output convs never take this path: see eligible())
       if (rs) gemm2_kernel<BM, BN, WM, WN, BK, S, true, false, true><<<grid, block, 0, s>>>(a, sp);
       else gemm2_kernel<BM, BN, WM, WN, BK, S, true, false, false><<<grid, block, 0, s>>>(a, sp);
     } else {
@@ -596,6 +719,8 @@ bool g_gemm_small = false;   // irx_set_option("gemm_small", 1): 4-wave 128x160 
 int g_gemm_small_kmax = 1280;
 bool g_splitk_inkernel = true;   // irx_set_option("splitk_inkernel", 0): separate split-K reduce kernel (A/B)
 bool g_tile_256x320 = true;      // irx_set_option("tile_256x320", 0): no 256x320 tiles (A/B)
+int g_conv_halo = 1;             // irx_set_option("conv_halo", m): 0 im2col walk for every conv (A/B),
+                                 // 1 halo tiles where the grid fills the chip, 2 wherever they fit (tests)
 int g_gemm_force = 0;            // irx_set_option("gemm_force", BM*100000 + BN*100 + splits): tuning sweeps
 
 bool gemm_geglu_fusable(const GemmArgs& a) {
@@ -603,17 +728,44 @@ bool gemm_geglu_fusable(const GemmArgs& a) {
   return choose(a).BM != 0;
 }
 
+int halo_bn(const GemmArgs& a);
+
 size_t gemm_workspace_bytes(const GemmArgs& a) {
-  if (!g_large_tiles || !eligible(a)) return 0;
+  if (!g_large_tiles || !eligible(a) || halo_bn(a)) return 0;
   const Choice c = choose(a);
   if (c.BM == 0 || c.splits <= 1) return 0;
   return (size_t)c.splits * a.batch * ((a.M + c.BM - 1) / c.BM * c.BM) * ((a.N + c.BN - 1) / c.BN * c.BN) *
          sizeof(float);
 }
 
+// Halo tile (BN) for a 3x3 / stride-1 / pad-1 conv whose 256-pixel tiles are whole image rows and whose
+// grid fills the chip; 0 = not applicable.
+int halo_bn(const GemmArgs& a) {
+  const ConvGeom& g = a.g;
+  if (!g_conv_halo || !a.conv || a.batch != 1 || a.geglu || a.out_f32 || !vec_ok(a)) return 0;
+  if (g.KH != 3 || g.KW != 3 || g.stride != 1 || g.pad_t != 1 || g.pad_l != 1) return 0;
+  if (g.Hv != g.Hin || g.Wv != g.Win || g.Ho != g.Hin || g.Wo != g.Win) return 0;
+  if (g.C0 % 64 || g.C1 % 64 || g.C0 <= 0) return 0;
+  const int W = g.Win;
+  if (W < 16 || W > kHaloWMax || (W & (W - 1)) || 256 % W || g.Hin % (256 / W)) return 0;
+  if ((long)g.N * g.Hin * W != a.M || a.M % 256) return 0;
+  const int bn = a.N % 160 == 0 ? 160 : 0;
+  if (!bn || (g_conv_halo < 2 && (long)(a.M / 256) * (a.N / bn) < kCUs)) return 0;
+  return bn;
+}
+
 // Returns false (caller uses the 4-wave kernel) when the shape does not fit the large-tile path.
 bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   if (!eligible(a)) return false;
+  if (const int hbn = halo_bn(a)) {
+    GemmArgs b = a;
+    b.vec_epilogue = 1;
+    b.dbg = g_gemm_dbg;
+    Split sp;
+    sp.per = a.K / 64;
+    launch2<256, 160, 4, 2, 64, 3, true>(b, sp, s);
+    return true;
+  }
   const Choice c = choose(a);
   if (c.BM == 0) return false;
   GemmArgs b = a;
