@@ -54,6 +54,7 @@ class StepParams(C.Structure):
 
 
 vp, i32, f32, sz, i64 = C.c_void_p, C.c_int, C.c_float, C.c_size_t, C.c_long
+u64 = C.c_ulonglong
 # name: (restype, argtypes); every status-returning function is checked
 _SIGS = {
     "irx_last_error": (C.c_char_p, []),
@@ -86,6 +87,10 @@ _SIGS = {
     "irx_latents_to_vae": (i32, [vp, i32, vp, i32, i32, i32, f32, vp]),
     "irx_image_to_tensor": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, vp]),
     "irx_tensor_to_image": (i32, [vp, i32, vp, i32, i32, i32, i32, vp, vp]),
+    "irx_degrade_noise": (i32, [vp, vp, i64, f32, vp, u64, vp]),
+    "irx_degrade_blur_down": (i32, [vp, vp, i32, i32, i32, i32, vp, i32, vp, vp]),
+    "irx_degrade_gray": (i32, [vp, vp, i64, i32, i32, vp]),
+    "irx_degrade_strokes": (i32, [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
     "irx_op_conv2d": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32,
                             i32, i32, i32, vp, i64, vp, vp, i32, i32]),
     "irx_op_gemm": (i32, [vp, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, f32, i32, vp, i64, i32, i32, i64,

@@ -277,6 +277,36 @@ int irx_tensor_to_image(void* s, int dtype, const void* x, int B, int H, int W, 
   IRX_API_END
 }
 
+// ------------------------------------------------------------------ synthetic degradations
+int irx_degrade_noise(void* s, const uint8_t* img, long n, float sigma, const float* noise, unsigned long long seed,
+                      uint8_t* out) {
+  IRX_API_BEGIN
+  IRX_CHECK(img && out && n >= 0, "bad arguments");
+  if (n) degrade_noise(img, out, n, sigma, noise, seed, S(s));
+  IRX_API_END
+}
+int irx_degrade_blur_down(void* s, const uint8_t* img, int batch, int H, int W, int C, const int* ksize, int scale,
+                          uint8_t* blur, uint8_t* lr) {
+  IRX_API_BEGIN
+  IRX_CHECK(img && ksize && blur && batch >= 0 && H > 0 && W > 0 && C > 0, "bad arguments");
+  IRX_CHECK(!lr || (scale >= 1 && H / scale > 0 && W / scale > 0), "bad scale");
+  if (batch) degrade_blur_down(img, batch, H, W, C, ksize, scale, blur, lr, S(s));
+  IRX_API_END
+}
+int irx_degrade_gray(void* s, const uint8_t* img, long npix, int mode, int rgb, uint8_t* out) {
+  IRX_API_BEGIN
+  IRX_CHECK(img && out && npix >= 0 && (mode == 0 || mode == 1), "bad arguments");
+  if (npix) degrade_gray(img, npix, mode, rgb, out, S(s));
+  IRX_API_END
+}
+int irx_degrade_strokes(void* s, int batch, int H, int W, const int* segs, const int* thick, const int* seg_off,
+                        uint8_t* mask, const uint8_t* img, uint8_t* masked) {
+  IRX_API_BEGIN
+  IRX_CHECK(seg_off && mask && batch >= 0 && H > 0 && W > 0, "bad arguments");
+  if (batch) degrade_strokes(batch, H, W, segs, thick, seg_off, mask, img, masked, S(s));
+  IRX_API_END
+}
+
 // ------------------------------------------------------------------ single ops
 int irx_op_conv2d(void* s, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hin, int win, int hv,
                   int wv, const void* weight, const float* bias, int cout, int kh, int kw, int stride, int pad_t,

@@ -136,4 +136,14 @@ void pack_unet_input(int dtype, const float* lat, int B, int h, int w, int cfg, 
 void scale_copy(int dtype_out, const float* in, long n, float scale, void* out, int in_ch, int out_ch,
                 hipStream_t s);
 
+
+// ------------------------------------------------------------ synthetic degradations (degrade.hip)
+void degrade_noise(const uint8_t* img, uint8_t* out, long n, float sigma, const float* z, unsigned long long seed,
+                   hipStream_t s);
+void degrade_blur_down(const uint8_t* img, int B, int H, int W, int C, const int* ksize_dev, int scale,
+                       uint8_t* blur, uint8_t* lr, hipStream_t s);
+void degrade_gray(const uint8_t* img, long npix, int mode, int rgb, uint8_t* out, hipStream_t s);
+void degrade_strokes(int B, int H, int W, const int* segs, const int* thick, const int* seg_off, uint8_t* mask,
+                     const uint8_t* img, uint8_t* masked, hipStream_t s);
+
 }  // namespace irx

@@ -141,6 +141,23 @@ int irx_image_to_tensor(void* stream, int dtype, const uint8_t* img, const float
 int irx_tensor_to_image(void* stream, int dtype, const void* x, int batch, int H, int W, int ldc, uint8_t* img,
                         float* f01);
 
+/* ---- synthetic degradations (scripts/make_synthetic_pairs.py) ----
+ * uint8 HWC batches in device memory, one pass each, no allocation. */
+/* add_gaussian_noise (make_synthetic_pairs.py:29-35): out = uint8(clip(f32(img) + f32(z) * sigma, 0, 255));
+ * z = `noise` (n floats, e.g. numpy's randn draws) or, if null, Philox4x32-10 normals keyed by `seed` */
+int irx_degrade_noise(void* stream, const uint8_t* img, long n, float sigma, const float* noise,
+                      unsigned long long seed, uint8_t* out);
+/* degrade_sr (:67-81): cv2.GaussianBlur(k, sigma 0) with k = ksize[b] in {3,5,7} (device int[batch]) into
+ * `blur` [batch][H][W][C]; if `lr`, cv2.resize(INTER_CUBIC) to [batch][H/scale][W/scale][C] */
+int irx_degrade_blur_down(void* stream, const uint8_t* img, int batch, int H, int W, int C, const int* ksize,
+                          int scale, uint8_t* blur, uint8_t* lr);
+/* to_grayscale (:84-90): mode 0 = cv2 BGR2GRAY, 1 = L of cv2 BGR2Lab; rgb != 0: input channel order R,G,B */
+int irx_degrade_gray(void* stream, const uint8_t* img, long npix, int mode, int rgb, uint8_t* out);
+/* random_free_form_mask (:104-114) + masked input (:196-198): segs int[nseg][4] (x0,y0,x1,y1), thick int[nseg],
+ * seg_off int[batch+1]; mask [batch][H][W] = 255 inside any stroke; img/masked (nullable) [batch][H][W][3] */
+int irx_degrade_strokes(void* stream, int batch, int H, int W, const int* segs, const int* thick, const int* seg_off,
+                        uint8_t* mask, const uint8_t* img, uint8_t* masked);
+
 /* ---- single-op entry points (parity tests, composition) ---- */
 int irx_op_conv2d(void* stream, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hin, int win,
                   int hv, int wv, const void* weight, const float* bias, int cout, int kh, int kw, int stride,
