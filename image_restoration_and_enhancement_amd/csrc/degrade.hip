@@ -70,25 +70,37 @@ __device__ __forceinline__ int reflect101(int i, int n) {
   return i;
 }
 
-// one output pixel-channel: sum_y w_y * (sum_x w_x * p) with integer weights (exact), round half up >> 16
+// Separable binomial blur through LDS: a block owns TW x TH output pixels of one image (all channels);
+// the (TH + 2r) x (TW + 2r) input tile is staged once, the exact integer row sums go to LDS, columns finish
+// in registers: sum_y w_y * (sum_x w_x * p), round half up >> 16 (integer weights: exact).
+constexpr int kBlurTW = 64, kBlurTH = 16, kBlurR = 3, kBlurCmax = 4;
 __global__ __launch_bounds__(256) void gauss_kernel(const uint8_t* __restrict__ img, uint8_t* __restrict__ out,
                                                     int B, int H, int W, int C, const int* __restrict__ ksize) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long n = (long)B * H * W * C;
-  if (i >= n) return;
-  const int c = (int)(i % C);
-  const long p = i / C;
-  const int x = (int)(p % W), y = (int)((p / W) % H), b = (int)(p / ((long)W * H));
+  __shared__ uint8_t tin[(kBlurTH + 2 * kBlurR) * (kBlurTW + 2 * kBlurR) * kBlurCmax];
+  __shared__ int th[(kBlurTH + 2 * kBlurR) * kBlurTW * kBlurCmax];
+  const int b = blockIdx.z, x0 = blockIdx.x * kBlurTW, y0 = blockIdx.y * kBlurTH;
   const int row = min(max(ksize[b] / 2, 0), 3), r = row;   // k in {1, 3, 5, 7} (others: clamped)
   const uint8_t* base = img + (long)b * H * W * C;
-  long acc = 0;
-  for (int dy = -r; dy <= r; ++dy) {
-    const int yy = reflect101(y + dy, H);
-    int h = 0;
-    for (int dx = -r; dx <= r; ++dx) h += c_gauss[row][dx + r] * base[((long)yy * W + reflect101(x + dx, W)) * C + c];
-    acc += (long)c_gauss[row][dy + r] * h;
+  const int IW = kBlurTW + 2 * r, IH = kBlurTH + 2 * r;
+  for (int e = threadIdx.x; e < IH * IW * C; e += blockDim.x) {
+    const int c = e % C, q = e / C, ix = q % IW, iy = q / IW;
+    tin[e] = base[((long)reflect101(y0 - r + iy, H) * W + reflect101(x0 - r + ix, W)) * C + c];
   }
-  out[i] = (uint8_t)min(255L, (acc + 32768) >> 16);
+  __syncthreads();
+  for (int e = threadIdx.x; e < IH * kBlurTW * C; e += blockDim.x) {
+    const int c = e % C, q = e / C, ox = q % kBlurTW, iy = q / kBlurTW;
+    int h = 0;
+    for (int j = 0; j <= 2 * r; ++j) h += c_gauss[row][j] * tin[(iy * IW + ox + j) * C + c];
+    th[e] = h;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kBlurTH * kBlurTW * C; e += blockDim.x) {
+    const int c = e % C, q = e / C, ox = q % kBlurTW, oy = q / kBlurTW;
+    if (x0 + ox >= W || y0 + oy >= H) continue;
+    long acc = 0;
+    for (int j = 0; j <= 2 * r; ++j) acc += (long)c_gauss[row][j] * th[((oy + j) * kBlurTW + ox) * C + c];
+    out[(((long)b * H + y0 + oy) * W + x0 + ox) * C + c] = (uint8_t)min(255L, (acc + 32768) >> 16);
+  }
 }
 
 // OpenCV INTER_CUBIC (A = -0.75), coefficients * 2048 rounded to short, horizontal int sums, vertical
@@ -134,9 +146,15 @@ __device__ __forceinline__ float srgb_lin(float v) {
   return v <= 0.04045f ? v * (1.f / 12.92f) : powf((v + 0.055f) * (1.f / 1.055f), 2.4f);
 }
 
-// mode 0: BGR2GRAY fixed point; mode 1: L of BGR2Lab.  rgb != 0: channel order R, G, B in memory.
+// mode 0: BGR2GRAY fixed point; mode 1: L of BGR2Lab (the sRGB linearisation of the 256 levels is
+// computed once per block into LDS).  rgb != 0: channel order R, G, B in memory.
 __global__ __launch_bounds__(256) void gray_kernel(const uint8_t* __restrict__ img, uint8_t* __restrict__ out,
                                                    long npix, int mode, int rgb) {
+  __shared__ float lin[256];
+  if (mode == 1) {
+    lin[threadIdx.x] = srgb_lin(threadIdx.x * (1.f / 255.f));
+    __syncthreads();
+  }
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= npix) return;
   const uint8_t c0 = img[i * 3], c1 = img[i * 3 + 1], c2 = img[i * 3 + 2];
@@ -145,35 +163,60 @@ __global__ __launch_bounds__(256) void gray_kernel(const uint8_t* __restrict__ i
     out[i] = (uint8_t)((R * 4899 + G * 9617 + Bc * 1868 + (1 << 13)) >> 14);
     return;
   }
-  const float Y = 0.212671f * srgb_lin(R * (1.f / 255.f)) + 0.715160f * srgb_lin(G * (1.f / 255.f)) +
-                  0.072169f * srgb_lin(Bc * (1.f / 255.f));
+  const float Y = 0.212671f * lin[R] + 0.715160f * lin[G] + 0.072169f * lin[Bc];
   const float L = Y > 0.008856f ? 116.f * cbrtf(Y) - 16.f : 903.3f * Y;
   out[i] = (uint8_t)fminf(fmaxf(rintf(L * 2.55f), 0.f), 255.f);
 }
 
-// segs: [nseg][4] (x0, y0, x1, y1), thick: [nseg], seg_off: [B+1] (image b owns segs seg_off[b] .. seg_off[b+1])
+// segs: [nseg][4] (x0, y0, x1, y1), thick: [nseg], seg_off: [B+1] (image b owns segs seg_off[b] .. seg_off[b+1]).
+// A block owns a 16 x 16 pixel tile: it first culls the image's segments to those whose bounding box,
+// grown by half the thickness, touches the tile (LDS list), then every pixel runs the exact capsule
+// test against that short list only.
+constexpr int kStrokeT = 16, kStrokeMaxList = 1024;
+__device__ __forceinline__ bool in_capsule(int x, int y, const int* sg, int t) {
+  // integer coordinates < 2^15: every product below is an integer < 2^53, exact in fp64 (and far cheaper
+  // than 64-bit integer multiplies)
+  const double x0 = sg[0], y0 = sg[1], x1 = sg[2], y1 = sg[3], tt = (double)t * t;
+  const double dx = x1 - x0, dy = y1 - y0, vx = x - x0, vy = y - y0;
+  const double L2 = dx * dx + dy * dy, dot = vx * dx + vy * dy;
+  if (L2 == 0.0 || dot <= 0.0) return 4.0 * (vx * vx + vy * vy) <= tt;
+  if (dot >= L2) {
+    const double ux = x - x1, uy = y - y1;
+    return 4.0 * (ux * ux + uy * uy) <= tt;
+  }
+  return 4.0 * ((vx * vx + vy * vy) * L2 - dot * dot) <= tt * L2;   // perpendicular distance^2 * L2
+}
+
 __global__ __launch_bounds__(256) void stroke_kernel(int B, int H, int W, const int* __restrict__ segs,
                                                      const int* __restrict__ thick, const int* __restrict__ seg_off,
                                                      uint8_t* __restrict__ mask, const uint8_t* __restrict__ img,
                                                      uint8_t* __restrict__ masked) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)B * H * W) return;
-  const int x = (int)(i % W), y = (int)((i / W) % H), b = (int)(i / ((long)W * H));
-  bool on = false;
-  for (int s = seg_off[b]; s < seg_off[b + 1] && !on; ++s) {
-    const long x0 = segs[4 * s], y0 = segs[4 * s + 1], x1 = segs[4 * s + 2], y1 = segs[4 * s + 3];
-    const long t = thick[s];
-    const long dx = x1 - x0, dy = y1 - y0, vx = x - x0, vy = y - y0;
-    const long L2 = dx * dx + dy * dy, dot = vx * dx + vy * dy;
-    if (L2 == 0 || dot <= 0) {
-      on = 4 * (vx * vx + vy * vy) <= t * t;
-    } else if (dot >= L2) {
-      const long ux = x - x1, uy = y - y1;
-      on = 4 * (ux * ux + uy * uy) <= t * t;
-    } else {   // perpendicular distance^2 = (|v|^2 L2 - dot^2) / L2
-      on = 4 * ((vx * vx + vy * vy) * L2 - dot * dot) <= t * t * L2;
+  __shared__ int list[kStrokeMaxList];
+  __shared__ int cnt;
+  const int b = blockIdx.z, tx0 = blockIdx.x * kStrokeT, ty0 = blockIdx.y * kStrokeT;
+  const int s0 = seg_off[b], s1 = seg_off[b + 1];
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  for (int sg = s0 + threadIdx.x; sg < s1; sg += blockDim.x) {
+    const int* p = segs + 4 * sg;
+    const int h = (thick[sg] + 1) / 2 + 1;
+    const int xl = min(p[0], p[2]) - h, xh = max(p[0], p[2]) + h, yl = min(p[1], p[3]) - h, yh = max(p[1], p[3]) + h;
+    if (xh >= tx0 && xl < tx0 + kStrokeT && yh >= ty0 && yl < ty0 + kStrokeT) {
+      const int k = atomicAdd(&cnt, 1);
+      if (k < kStrokeMaxList) list[k] = sg;
     }
   }
+  __syncthreads();
+  const int x = tx0 + (threadIdx.x & (kStrokeT - 1)), y = ty0 + threadIdx.x / kStrokeT;
+  if (x >= W || y >= H) return;
+  const int n = cnt;
+  bool on = false;
+  if (n <= kStrokeMaxList) {
+    for (int k = 0; k < n && !on; ++k) on = in_capsule(x, y, segs + 4 * list[k], thick[list[k]]);
+  } else {
+    for (int sg = s0; sg < s1 && !on; ++sg) on = in_capsule(x, y, segs + 4 * sg, thick[sg]);
+  }
+  const long i = ((long)b * H + y) * W + x;
   mask[i] = on ? 255 : 0;
   if (img && masked) {
 #pragma unroll
@@ -194,8 +237,9 @@ void degrade_noise(const uint8_t* img, uint8_t* out, long n, float sigma, const 
 
 void degrade_blur_down(const uint8_t* img, int B, int H, int W, int C, const int* ksize_dev, int scale,
                        uint8_t* blur, uint8_t* lr, hipStream_t s) {
-  const long n = (long)B * H * W * C;
-  gauss_kernel<<<blocks(n), 256, 0, s>>>(img, blur, B, H, W, C, ksize_dev);
+  IRX_CHECK(C <= kBlurCmax, "at most 4 channels");
+  gauss_kernel<<<dim3((W + kBlurTW - 1) / kBlurTW, (H + kBlurTH - 1) / kBlurTH, B), 256, 0, s>>>(img, blur, B, H, W,
+                                                                                                  C, ksize_dev);
   IRX_LAUNCH_CHECK();
   if (lr && scale >= 1) {
     const int Ho = H / scale, Wo = W / scale;
@@ -211,7 +255,8 @@ void degrade_gray(const uint8_t* img, long npix, int mode, int rgb, uint8_t* out
 
 void degrade_strokes(int B, int H, int W, const int* segs, const int* thick, const int* seg_off, uint8_t* mask,
                      const uint8_t* img, uint8_t* masked, hipStream_t s) {
-  stroke_kernel<<<blocks((long)B * H * W), 256, 0, s>>>(B, H, W, segs, thick, seg_off, mask, img, masked);
+  stroke_kernel<<<dim3((W + kStrokeT - 1) / kStrokeT, (H + kStrokeT - 1) / kStrokeT, B), 256, 0, s>>>(
+      B, H, W, segs, thick, seg_off, mask, img, masked);
   IRX_LAUNCH_CHECK();
 }
 

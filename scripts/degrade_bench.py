@@ -39,13 +39,25 @@ lr = torch.empty((B, H // 4, W // 4, 3), dtype=torch.uint8, device=dev)
 random.seed(0)
 strokes = [D.draw_free_form_strokes(H, W, (8, 15), (20, 40)) for _ in range(B)]
 S, P = D._s, D._p
+segs, thick, off = [], [], [0]
+for st in strokes:
+    for pts, t in st:
+        for (x0, y0), (x1, y1) in zip(pts[:-1], pts[1:]):
+            segs.append((x0, y0, x1, y1))
+            thick.append(t)
+    off.append(len(segs))
+sg = torch.tensor(segs, dtype=torch.int32, device=dev)
+th = torch.tensor(thick, dtype=torch.int32, device=dev)
+of = torch.tensor(off, dtype=torch.int32, device=dev)
+mask = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
 rows = [
     ("noise (in-kernel Philox)", lambda: L.call("irx_degrade_noise", S(), P(x), n, 6.0, None, 1, P(out)), 2 * n),
     ("noise (given fp32 draws)", lambda: L.call("irx_degrade_noise", S(), P(x), n, 6.0, P(z), 0, P(out)), 6 * n),
     ("gauss 7x7 + cubic /4", lambda: L.call("irx_degrade_blur_down", S(), P(x), B, H, W, 3, P(ks), 4, P(blur), P(lr)),
      3 * n + n // 16),
     ("gray lab", lambda: L.call("irx_degrade_gray", S(), P(x), n // 3, 1, 0, P(gray)), n + n // 3),
-    ("strokes + masked", lambda: D.rasterize_strokes(H, W, strokes, dev, x), n // 3 + 2 * n),
+    ("strokes + masked", lambda: L.call("irx_degrade_strokes", S(), B, H, W, P(sg), P(th), P(of), P(mask), P(x),
+                                        P(out)), n // 3 + 2 * n),
 ]
 for name, fn, byt in rows:
     t = timeit(fn)
