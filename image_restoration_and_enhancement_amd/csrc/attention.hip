@@ -296,8 +296,11 @@ __global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
   // QK^T contracts over DQ = 32 * NDC (head dim zero-padded).  (A 16x16x16 MFMA for a d % 32 == 8..16 tail was
   // tried: hipcc (ROCm 7.2) issues it right behind the 16x16x32 producing its accumulator with no wait states,
   // and the result is wrong — mixed-shape MFMA accumulation chains are avoided here.)
+  // DQ % 32 == 16 (d = 40 -> 48): the last 16 dims go through one 16x16x16 MFMA into a SEPARATE
+  // accumulator that the VALU adds to S (no mixed-shape MFMA chain), instead of padding d to 64.
   constexpr int NDC = DQ / 32, NDT = DV / 16, NKT = KT / 16, NKC = KT / 32;
-  static_assert(DQ % 32 == 0, "head dim padding");
+  constexpr bool TAIL = DQ % 32 == 16;
+  static_assert(DQ % 32 == 0 || TAIL, "head dim padding");
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[KT * SK];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[KT * SV];
@@ -316,6 +319,7 @@ __global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
   for (int i = tid; i < KT * SV; i += 256) Vs[i] = (ONES && i % SV == a.d) ? (bf16_t)0x3F80 : (bf16_t)0;
 
   s16x8 qf[kQT][NDC];
+  s16x4 qtl[kQT];
 #pragma unroll
   for (int qt = 0; qt < kQT; ++qt) {
     const int q = q0 + qt * 16 + li;
@@ -325,6 +329,11 @@ __global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
       s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
       if (q < a.Lq && e < d) v = *(const s16x8*)(Q + (long)q * a.ldq + e);
       qf[qt][dc] = v;
+    }
+    qtl[qt] = s16x4{0, 0, 0, 0};
+    if constexpr (TAIL) {
+      const int e = NDC * 32 + 4 * g;
+      if (q < a.Lq && e < d) qtl[qt] = *(const s16x4*)(Q + (long)q * a.ldq + e);
     }
   }
   f32x4 o[NDT][kQT];
@@ -387,6 +396,14 @@ __global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
         for (int qt = 0; qt < kQT; ++qt)
           s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf),
                                                               __builtin_bit_cast(bf16x8, qf[qt][dc]), s[kt][qt], 0, 0, 0);
+      }
+      if constexpr (TAIL) {
+        const s16x4 kt4 = *(const s16x4*)(Ks + (kt * 16 + li) * SK + NDC * 32 + 4 * g);
+#pragma unroll
+        for (int qt = 0; qt < kQT; ++qt) {
+          const f32x4 t = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kt4, qtl[qt], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          s[kt][qt] += t;
+        }
       }
     }
 
@@ -487,6 +504,7 @@ void launch_bf16(const AttnArgs& a, hipStream_t s) {
   const char* inst = a.d == 40 ? (g_attn_d40 == 1   ? "64, 48, 128, false"
                                   : g_attn_d40 == 2 ? "64, 48, 64, true, 3"
                                   : g_attn_d40 == 3 ? "64, 48, 64, true, 4"
+                                  : g_attn_d40 == 4 ? "48, 48, 64, true, 3"
                                                     : "64, 48, 128, true, 2")
                      : a.d == 64 ? "64, 64, 128, false"
                      : a.d == 80 ? "96, 80, 64, false" : "160, 160, 32, false";
@@ -497,6 +515,7 @@ void launch_bf16(const AttnArgs& a, hipStream_t s) {
       if (g_attn_d40 == 1) attn2_kernel<64, 48, 128, false><<<grid, block, 0, s>>>(a);
       else if (g_attn_d40 == 2) attn2_kernel<64, 48, 64, true, 3><<<grid, block, 0, s>>>(a);
       else if (g_attn_d40 == 3) attn2_kernel<64, 48, 64, true, 4><<<grid, block, 0, s>>>(a);
+      else if (g_attn_d40 == 4) attn2_kernel<48, 48, 64, true, 3><<<grid, block, 0, s>>>(a);
       else attn2_kernel<64, 48, 128, true><<<grid, block, 0, s>>>(a);
       break;
     case 64: attn2_kernel<64, 64, 128, false><<<grid, block, 0, s>>>(a); break;

@@ -357,3 +357,20 @@ def test_conv_halo(device, halo_forced, case):
     if extra:
         ref = ref + _q(res, dt)
     assert O.rel_err(got, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("B,Lq,Lk", [(2, 256, 256), (2, 200, 77), (1, 333, 190)])
+def test_attention_d40_variants(device, variant, B, Lq, Lk):
+    """Every d = 40 bf16 kernel variant (irx_set_option("attn_d40")): 128 / 64-key tiles, ones-column or
+    VALU row sums, d padded to 64 or to 48 with a 16x16x16 tail MFMA."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    dt = torch.bfloat16
+    q, k, v = _r(B, Lq, 320, seed=60), _r(B, Lk, 320, seed=61), _r(B, Lk, 320, seed=62)
+    L.call("irx_set_option", b"attn_d40", variant)
+    try:
+        got = O.attention(_dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device), 8)
+    finally:
+        L.call("irx_set_option", b"attn_d40", 2)
+    ref = O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), 8)
+    assert O.rel_err(got, ref) < 2 * TOL[dt]
