@@ -280,6 +280,15 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
   }
 }
 
+// max over lanes {i, i^16, i^32, i^48} with gfx950's v_permlane16/32_swap (VALU, no LDS round trip as
+// ds_bpermute would take): swapping a value with itself leaves each lane holding its partner's copy
+__device__ __forceinline__ float quad_max(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
 // ------------------------------------------------------------------------------------------------
 // bf16 throughput kernel: v_mfma_f32_16x16x32_bf16 for both products.
 //   S^T = K Q^T : K fragments by ds_read_b128 (d padded to DQ, a multiple of 32), Q^T in registers.
@@ -425,8 +434,7 @@ __global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt)
         tmax = fmaxf(tmax, fmaxf(fmaxf(s[kt][qt][0], s[kt][qt][1]), fmaxf(s[kt][qt][2], s[kt][qt][3])));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      tmax = quad_max(tmax);
       const float mnew = fmaxf(mrow[qt], tmax);
       const bool none = mnew == -INFINITY;
       const float alpha = none ? 1.f : __builtin_amdgcn_exp2f((mrow[qt] - mnew) * sl2);
