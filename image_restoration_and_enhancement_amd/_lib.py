@@ -91,6 +91,8 @@ _SIGS = {
     "irx_degrade_blur_down": (i32, [vp, vp, i32, i32, i32, i32, vp, i32, vp, vp]),
     "irx_degrade_gray": (i32, [vp, vp, i64, i32, i32, vp]),
     "irx_degrade_strokes": (i32, [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+    "irx_nlm_weights": (i32, [f32, i32, i32, i32, C.POINTER(i32), i32, C.POINTER(i32)]),
+    "irx_nlmeans_u8": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32]),
     "irx_op_conv2d": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32,
                             i32, i32, i32, vp, i64, vp, vp, i32, i32]),
     "irx_op_gemm": (i32, [vp, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, f32, i32, vp, i64, i32, i32, i64,

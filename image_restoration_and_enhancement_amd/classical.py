@@ -5,9 +5,10 @@ cv2 is not installed on this image (neither here nor on the GPU box), so these a
 OpenCV's documented algorithms; where OpenCV uses a private approximation the result may differ by a
 few uint8 levels — parity unpinned (no oracle available), except where stated "exact":
 
-* `denoise_opencv`   — src/inference.py:500-522: fastNlMeansDenoisingColored(h, hColor, 7, 21) (non-local
-                       means in 8-bit CIELAB, L with h, a/b with hColor), then bilateralFilter(9, 75, 75)
-                       if strength > 0.6 and medianBlur(5) if strength > 0.8.
+* `denoise_opencv`   — src/inference.py:500-522: fastNlMeansDenoisingColored(h, hColor, 7, 21) (OpenCV's
+                       integer NLM invoker, exact given the Lab bytes, on 8-bit LBGR-Lab: L with h, the a/b
+                       pair with hColor; the GPU form is `nlmeans` / csrc/nlmeans.hip), then
+                       bilateralFilter(9, 75, 75) if strength > 0.6 and medianBlur(5) if strength > 0.8.
 * `sr_lanczos`       — src/inference.py:593-596: PIL LANCZOS resize (exact: same library call).
 * `colorize_lab`     — src/inference.py:683-703: L of RGB->LAB, a = L*0.1-10, b = L*0.1-5 as int8
                        (negative values wrap through the uint8 cast exactly as the reference's
@@ -36,10 +37,12 @@ def rgb_to_gray_u8(rgb: np.ndarray) -> np.ndarray:
     return ((r * 4899 + g * 9617 + b * 1868 + (1 << 13)) >> 14).astype(np.uint8)
 
 
-def rgb_to_lab_u8(rgb: np.ndarray) -> np.ndarray:
-    """8-bit CIELAB as OpenCV stores it: L*255/100, a+128, b+128 (float arithmetic, rounded)."""
+def rgb_to_lab_u8(rgb: np.ndarray, srgb: bool = True) -> np.ndarray:
+    """8-bit CIELAB as OpenCV stores it: L*255/100, a+128, b+128 (float arithmetic, rounded).
+    srgb=False: the L-variants (COLOR_LRGB2Lab), no gamma linearisation."""
     x = rgb.astype(np.float64) / 255.0
-    x = np.where(x > 0.04045, ((x + 0.055) / 1.055) ** 2.4, x / 12.92)
+    if srgb:
+        x = np.where(x > 0.04045, ((x + 0.055) / 1.055) ** 2.4, x / 12.92)
     xyz = x @ _M_RGB2XYZ.T / _WHITE
     f = np.where(xyz > 0.008856, np.cbrt(xyz), 7.787 * xyz + 16.0 / 116.0)
     L = np.where(xyz[..., 1] > 0.008856, 116.0 * f[..., 1] - 16.0, 903.3 * xyz[..., 1])
@@ -49,7 +52,17 @@ def rgb_to_lab_u8(rgb: np.ndarray) -> np.ndarray:
     return np.clip(np.rint(out), 0, 255).astype(np.uint8)
 
 
-def lab_u8_to_rgb(lab: np.ndarray) -> np.ndarray:
+def lbgr_to_lab_u8(img: np.ndarray) -> np.ndarray:
+    """cv2.COLOR_LBGR2Lab as fastNlMeansDenoisingColored applies it: channel 0 is taken as blue."""
+    return rgb_to_lab_u8(img[..., ::-1], srgb=False)
+
+
+def lab_u8_to_lbgr(lab: np.ndarray) -> np.ndarray:
+    """cv2.COLOR_Lab2LBGR (the inverse of lbgr_to_lab_u8)."""
+    return np.ascontiguousarray(lab_u8_to_rgb(lab, srgb=False)[..., ::-1])
+
+
+def lab_u8_to_rgb(lab: np.ndarray, srgb: bool = True) -> np.ndarray:
     L = lab[..., 0].astype(np.float64) * 100.0 / 255.0
     a = lab[..., 1].astype(np.float64) - 128.0
     b = lab[..., 2].astype(np.float64) - 128.0
@@ -63,7 +76,8 @@ def lab_u8_to_rgb(lab: np.ndarray) -> np.ndarray:
     xyz = np.stack([finv(fx), y, finv(fz)], -1) * _WHITE
     rgb = xyz @ np.linalg.inv(_M_RGB2XYZ).T
     rgb = np.clip(rgb, 0.0, 1.0)
-    rgb = np.where(rgb > 0.0031308, 1.055 * rgb ** (1 / 2.4) - 0.055, 12.92 * rgb)
+    if srgb:
+        rgb = np.where(rgb > 0.0031308, 1.055 * rgb ** (1 / 2.4) - 0.055, 12.92 * rgb)
     return np.clip(np.rint(rgb * 255.0), 0, 255).astype(np.uint8)
 
 
@@ -77,25 +91,59 @@ def _box_sum(x: np.ndarray, r: int) -> np.ndarray:
     return c[k:, k:] - c[:-k, k:] - c[k:, :-k] + c[:-k, :-k]
 
 
-def nl_means(img: np.ndarray, h: np.ndarray, template: int = 7, search: int = 21) -> np.ndarray:
-    """Non-local means over a [H, W, C] float image; per-channel filter strength h[C]:
-    w(p, q) = exp(-sum_c mean_patch (I_c(p) - I_c(q))^2 / h_c^2 / C)."""
-    H, W, C = img.shape
+def nlm_weights(h: float, cn: int, template: int = 7, search: int = 21) -> np.ndarray:
+    """OpenCV FastNlMeansDenoisingInvoker's weight table: w[a] = cvRound(fpm * exp(-a * 2^s / template^2 /
+    (f32(h)^2 * cn))), zero below 0.001 * fpm, fpm = INT_MAX // (search^2 * 255), 2^s >= template^2."""
+    s = max(int(np.ceil(np.log2(template * template))), 0)
+    mult = float(1 << s) / (template * template)
+    fpm = (2 ** 31 - 1) // (search * search * 255)
+    hf = np.float32(h)
+    den = float(np.float32(np.float32(hf * hf) * np.float32(cn)))
+    d = np.arange(int(255 * 255 * cn / mult + 1), dtype=np.float64) * mult
+    with np.errstate(divide="ignore", invalid="ignore"):
+        w = np.exp(-d / den)
+    w = np.where(np.isnan(w), 1.0, w)
+    wi = np.rint(fpm * w).astype(np.int64)
+    wi[wi < 0.001 * fpm] = 0
+    return wi
+
+
+def nl_means_u8(img: np.ndarray, h: float, template: int = 7, search: int = 21) -> np.ndarray:
+    """cv2.fastNlMeansDenoising's invoker on a uint8 [H, W, cn] channel group (exact integer arithmetic):
+    patch SSD summed over the group, weight = table[SSD >> s], rounded integer weighted mean; reflect-101
+    borders.  The CPU form of csrc/nlmeans.hip (used on hosts without a GPU)."""
+    H, W, cn = img.shape
     tr, sr = template // 2, search // 2
-    pad = np.pad(img, ((sr, sr), (sr, sr), (0, 0)), mode="reflect")
-    inv_h2 = 1.0 / np.maximum(np.asarray(h, np.float64) ** 2, 1e-12)
-    acc = np.zeros_like(img, dtype=np.float64)
-    wsum = np.zeros((H, W), np.float64)
-    area = float(template * template)
+    b = tr + sr
+    ext = np.pad(img, ((b, b), (b, b), (0, 0)), mode="reflect").astype(np.int64)
+    lut = nlm_weights(h, cn, template, search)
+    s = max(int(np.ceil(np.log2(template * template))), 0)
+    ctr = ext[sr:sr + H + 2 * tr, sr:sr + W + 2 * tr]
+    est = np.zeros((H, W, cn), np.int64)
+    wsum = np.zeros((H, W), np.int64)
     for dy in range(-sr, sr + 1):
         for dx in range(-sr, sr + 1):
-            sh = pad[sr + dy:sr + dy + H, sr + dx:sr + dx + W]
-            d2 = ((img - sh) ** 2 * inv_h2).sum(-1) / C
-            dist = _box_sum(d2, tr) / area
-            w = np.exp(-np.maximum(dist, 0.0))
-            acc += w[..., None] * sh
+            d = ((ctr - ext[sr + dy:sr + dy + H + 2 * tr, sr + dx:sr + dx + W + 2 * tr]) ** 2).sum(-1)
+            dist = _box_sum_valid(d, template)
+            w = lut[dist >> s]
             wsum += w
-    return acc / wsum[..., None]
+            est += w[..., None] * ext[b + dy:b + dy + H, b + dx:b + dx + W]
+    return np.clip((est + (wsum // 2)[..., None]) // wsum[..., None], 0, 255).astype(np.uint8)
+
+
+def _box_sum_valid(x: np.ndarray, k: int) -> np.ndarray:
+    c = np.pad(x.cumsum(0).cumsum(1), ((1, 0), (1, 0)))
+    return c[k:, k:] - c[:-k, k:] - c[k:, :-k] + c[:-k, :-k]
+
+
+def fast_nl_means_denoising_colored(img: np.ndarray, h: float, h_color: float, template: int = 7,
+                                    search: int = 21) -> np.ndarray:
+    """cv2.fastNlMeansDenoisingColored (denoising.cpp): LBGR -> 8-bit Lab, L with h, (a, b) with hColor, back."""
+    lab = lbgr_to_lab_u8(img)
+    out = np.empty_like(lab)
+    out[..., :1] = nl_means_u8(lab[..., :1], h, template, search)
+    out[..., 1:] = nl_means_u8(lab[..., 1:], h_color, template, search)
+    return lab_u8_to_lbgr(out)
 
 
 def bilateral(img: np.ndarray, d: int = 9, sigma_color: float = 75.0, sigma_space: float = 75.0) -> np.ndarray:
@@ -127,14 +175,14 @@ def median5(img: np.ndarray) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------------------- tasks
-def denoise_opencv(image: Image.Image, strength: float) -> Image.Image:
+def denoise_opencv(image: Image.Image, strength: float, nlm=None) -> Image.Image:
+    """src/inference.py:500-522.  `nlm` = the fastNlMeansDenoisingColored implementation (the GPU one from
+    `nlmeans` on a ROCm device; this module's numpy form otherwise)."""
     img = np.array(image.convert("RGB"))
     hs = float(np.clip(strength, 0.1, 1.0))
     h_value = hs * 10 if hs < 0.6 else 20          # luminance strength
     h_color = hs * 10 if hs < 0.6 else 20          # chroma strength (same rule in the reference)
-    lab = rgb_to_lab_u8(img).astype(np.float64)
-    out = nl_means(lab, np.array([h_value, h_color, h_color]))
-    den = lab_u8_to_rgb(np.clip(np.rint(out), 0, 255).astype(np.uint8))
+    den = (nlm or fast_nl_means_denoising_colored)(img, h_value, h_color, 7, 21)
     if strength > 0.6:
         den = bilateral(den, 9, 75, 75)
     if strength > 0.8:

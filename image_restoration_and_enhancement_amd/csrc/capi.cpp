@@ -1,6 +1,8 @@
 // irx — extern "C" boundary (include/irx.h).  Every entry point catches C++ exceptions and turns
 // them into a non-zero status plus a thread-local message, so the Python layer can log and fall
 // back the way src/inference.py does around its diffusers calls.
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <string>
 
@@ -304,6 +306,45 @@ int irx_degrade_strokes(void* s, int batch, int H, int W, const int* segs, const
   IRX_API_BEGIN
   IRX_CHECK(seg_off && mask && batch >= 0 && H > 0 && W > 0, "bad arguments");
   if (batch) degrade_strokes(batch, H, W, segs, thick, seg_off, mask, img, masked, S(s));
+  IRX_API_END
+}
+
+// ------------------------------------------------------------------ fast non-local means
+static int nlm_shift(int tmpl) {
+  int s = 0;
+  while ((1 << s) < tmpl * tmpl) ++s;
+  return s;
+}
+int irx_nlm_weights(float h, int cn, int tmpl, int search, int* lut, int cap, int* lut_len) {
+  IRX_API_BEGIN
+  IRX_CHECK(lut_len && cn >= 1 && cn <= 4 && tmpl >= 1 && (tmpl & 1) && search >= 1 && (search & 1), "bad arguments");
+  // FastNlMeansDenoisingInvoker's constructor + DistSquared::calcWeight (OpenCV 4.x, uint8 / int)
+  const int tws2 = tmpl * tmpl, shift = nlm_shift(tmpl);
+  const double mult = (double)(1 << shift) / tws2;
+  const int fpm = (int)std::min<long>(2147483647L / ((long)search * search * 255), 2147483647L);
+  const int almost_max = (int)(255.0 * 255.0 * cn / mult + 1);
+  const float den = h * h * (float)cn;
+  int n = 0;
+  for (; n < almost_max; ++n) {
+    double w = std::exp(-(n * mult) / den);
+    if (std::isnan(w)) w = 1.0;
+    int wt = (int)std::nearbyint(fpm * w);
+    if (wt < 0.001 * fpm) wt = 0;
+    if (wt == 0) break;                     // non-increasing in n: the rest of the table is zero
+    if (lut) {
+      IRX_CHECK(n < cap, "weight table capacity too small");
+      lut[n] = wt;
+    }
+  }
+  *lut_len = n;
+  IRX_API_END
+}
+int irx_nlmeans_u8(void* s, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int pix_stride, int ch_off,
+                   int cn, int tmpl, int search, const int* lut, int lut_len) {
+  IRX_API_BEGIN
+  IRX_CHECK(src && dst && src != dst && lut && lut_len >= 1 && batch >= 0 && H > 0 && W > 0, "bad arguments");
+  IRX_CHECK(ch_off >= 0 && ch_off + cn <= pix_stride, "channel group outside the pixel");
+  if (batch) nlmeans_u8(src, dst, batch, H, W, pix_stride, ch_off, cn, tmpl, search, lut, lut_len, nlm_shift(tmpl), S(s));
   IRX_API_END
 }
 

@@ -1,0 +1,169 @@
+// irx — OpenCV's fast non-local-means denoiser (the invoker behind cv2.fastNlMeansDenoisingColored, which the
+// reference's classical denoise fallback calls: src/inference.py:509-515) on uint8 batches
+// resident in HBM.  Integer-exact restatement of FastNlMeansDenoisingInvoker (oracle/nlm_ref.py):
+//   dist(p, q) = sum_{template} sum_c (I_c(p+t) - I_c(q+t))^2,  w = lut[min(dist >> shift, lut_len)],
+//   out_c = (sum_q w I_c(q) + W/2) / W over the search window, BORDER_REFLECT_101 everywhere.
+// The weight table is built on the host (irx_nlm_weights) and staged once per block in LDS.
+//
+// Work decomposition: one block per 32x32 output tile and image; its (32+2B)^2 reflect-padded region
+// (B = search/2 + template/2) of the channel group sits in LDS (bytes; a 2-channel group as 16-bit pairs so
+// one v_pk_sub_i16 + v_dot2_i32_i16 forms a tap's two-channel squared distance).  Each thread owns a column strip of
+// 4 pixels and keeps the strip's own template rows in registers.  For each search row offset it slides a
+// (4+2r) x (2r+1) register window of the neighbour rows across the 2s+1 column offsets, loading one new LDS
+// column per offset.  Row SSDs are formed once per strip row and summed into the 4 pixel distances, which is
+// 4x fewer squared differences than per-pixel templates.  Compute (VALU) bound: HBM traffic is one read and
+// one write of the image.
+#include "ops.h"
+#include "profile.h"
+
+#include <type_traits>
+
+namespace irx {
+namespace {
+
+constexpr int NLM_TW = 32, NLM_S = 4, NLM_G = 8, NLM_TH = NLM_S * NLM_G;   // 32x32 tile, 256 threads
+
+__device__ __forceinline__ int refl101(int p, int n) {
+  if (n == 1) return 0;
+  while ((unsigned)p >= (unsigned)n) p = p < 0 ? -p : 2 * (n - 1) - p;
+  return p;
+}
+
+typedef short nlm_s2 __attribute__((ext_vector_type(2)));
+
+// squared distance of one tap: CN 1 = one byte; CN 2 = both channels packed as 16-bit halves (lo = c0,
+// hi = c1), one v_pk_sub_i16 + one v_dot2 per tap
+template <int CN>
+__device__ __forceinline__ int tap(int s, int o, int n) {
+  if constexpr (CN == 1) {
+    const int d = o - n;
+    return s + d * d;
+  } else {
+    const nlm_s2 d = __builtin_bit_cast(nlm_s2, o) - __builtin_bit_cast(nlm_s2, n);
+    return __builtin_amdgcn_sdot2(d, d, s, false);
+  }
+}
+
+template <int CN, int TR, int SR>
+__global__ __launch_bounds__(256) void nlm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                  int H, int W, int ps, int coff, const int* __restrict__ lut,
+                                                  int lut_len, int shift) {
+  static_assert(CN == 1 || CN == 2, "channel groups of 1 or 2");
+  using PV = typename std::conditional<CN == 1, uint8_t, uint32_t>::type;
+  constexpr int B = TR + SR, T = 2 * TR + 1, RH = NLM_TH + 2 * B, RW = NLM_TW + 2 * B, NR = NLM_S + 2 * TR;
+  constexpr int PLANE = RH * RW;
+  extern __shared__ int smem[];
+  PV* reg = reinterpret_cast<PV*>(smem);                      // [RH][RW] pixels of the group
+  int* wl = smem + (PLANE * (int)sizeof(PV) + 3) / 4;         // [lut_len + 1], last entry 0
+  const int tid = threadIdx.x, x0 = blockIdx.x * NLM_TW, y0 = blockIdx.y * NLM_TH;
+  const uint8_t* img = src + (size_t)blockIdx.z * H * W * ps + coff;
+  for (int i = tid; i < PLANE; i += 256) {
+    const int ry = i / RW, rx = i - ry * RW;
+    const uint8_t* p = img + ((size_t)refl101(y0 + ry - B, H) * W + refl101(x0 + rx - B, W)) * ps;
+    if constexpr (CN == 1) reg[i] = p[0];
+    else reg[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 16);
+  }
+  for (int i = tid; i <= lut_len; i += 256) wl[i] = i < lut_len ? lut[i] : 0;
+  __syncthreads();
+
+  const int col = tid & (NLM_TW - 1), grp = tid / NLM_TW;
+  int own[NR][T];                                             // template rows of the strip (registers)
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int k = 0; k < T; ++k) own[j][k] = (int)reg[(grp * NLM_S + SR + j) * RW + col + SR + k];
+
+  int wsum[NLM_S], est[NLM_S][CN];
+#pragma unroll
+  for (int i = 0; i < NLM_S; ++i) {
+    wsum[i] = 0;
+#pragma unroll
+    for (int c = 0; c < CN; ++c) est[i][c] = 0;
+  }
+
+  for (int a = 0; a <= 2 * SR; ++a) {                         // search row offset dy = a - SR
+    const PV* rb = reg + (grp * NLM_S + a) * RW + col;
+    int nb[NR][T];
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int k = 0; k < T - 1; ++k) nb[j][k] = (int)rb[j * RW + k];
+#pragma unroll
+    for (int b = 0; b <= 2 * SR; ++b) {                       // search column offset dx = b - SR
+#pragma unroll
+      for (int j = 0; j < NR; ++j) nb[j][T - 1] = (int)rb[j * RW + b + T - 1];
+      int R[NR];
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        int s = 0;
+#pragma unroll
+        for (int k = 0; k < T; ++k) s = tap<CN>(s, own[j][k], nb[j][k]);
+        R[j] = s;
+      }
+#pragma unroll
+      for (int i = 0; i < NLM_S; ++i) {
+        int dist = 0;
+#pragma unroll
+        for (int t = 0; t < T; ++t) dist += R[i + t];
+        const int w = wl[min(dist >> shift, lut_len)];
+        wsum[i] += w;
+        const int q = nb[i + TR][TR];
+        if constexpr (CN == 1) {
+          est[i][0] += w * q;
+        } else {
+          est[i][0] += w * (q & 0xffff);
+          est[i][1] += w * (q >> 16);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int k = 0; k < T - 1; ++k) nb[j][k] = nb[j][k + 1];
+    }
+  }
+
+  const int x = x0 + col;
+#pragma unroll
+  for (int i = 0; i < NLM_S; ++i) {
+    const int y = y0 + grp * NLM_S + i;
+    if (y < H && x < W) {
+      uint8_t* o = dst + (((size_t)blockIdx.z * H + y) * W + x) * ps + coff;
+      const unsigned ws = (unsigned)wsum[i];                  // > 0: the centre offset weighs fpm
+#pragma unroll
+      for (int c = 0; c < CN; ++c) o[c] = (uint8_t)min(255u, ((unsigned)est[i][c] + ws / 2) / ws);
+    }
+  }
+}
+
+template <int CN, int TR, int SR>
+void launch(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, const int* lut, int lut_len,
+            int shift, hipStream_t s) {
+  constexpr int B = TR + SR, PLANE = (NLM_TH + 2 * B) * (NLM_TW + 2 * B), PB = CN == 1 ? 1 : 4;
+  const size_t lds = ((PLANE * PB + 3) / 4 + lut_len + 1) * sizeof(int);
+  IRX_CHECK(lds <= 160 * 1024, "nlmeans: weight table too long for LDS (h too large)");
+  auto k = nlm_kernel<CN, TR, SR>;
+  if (lds > 64 * 1024) IRX_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)lds));
+  const dim3 grid((W + NLM_TW - 1) / NLM_TW, (H + NLM_TH - 1) / NLM_TH, N);
+  // algorithmic integer ops of the direct form: (sub, mul, add) per template tap, channel and search offset
+  const double ops = 3.0 * N * H * W * (2 * SR + 1) * (2 * SR + 1) * (2 * TR + 1) * (2 * TR + 1) * CN;
+  ProfScope pr(prof_on() ? std::string("irx::(anonymous namespace)::nlm_kernel") : std::string(), ops, s);
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, src, dst, H, W, ps, coff, lut, lut_len, shift);
+  IRX_HIP(hipGetLastError());
+}
+
+}  // namespace
+
+void nlmeans_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, int cn, int tmpl,
+                int search, const int* lut, int lut_len, int shift, hipStream_t s) {
+  if (tmpl == 7 && search == 21) {
+    if (cn == 1) return launch<1, 3, 10>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+    if (cn == 2) return launch<2, 3, 10>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+  } else if (tmpl == 3 && search == 5) {
+    if (cn == 1) return launch<1, 1, 2>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+    if (cn == 2) return launch<2, 1, 2>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+  }
+  IRX_CHECK(false, "nlmeans: supported (template, search, cn): (7, 21) and (3, 5) with cn 1 or 2");
+}
+
+}  // namespace irx

@@ -146,4 +146,9 @@ void degrade_gray(const uint8_t* img, long npix, int mode, int rgb, uint8_t* out
 void degrade_strokes(int B, int H, int W, const int* segs, const int* thick, const int* seg_off, uint8_t* mask,
                      const uint8_t* img, uint8_t* masked, hipStream_t s);
 
+
+// ------------------------------------------------------------ fast non-local means (nlmeans.hip)
+void nlmeans_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, int cn, int tmpl,
+                int search, const int* lut, int lut_len, int shift, hipStream_t s);
+
 }  // namespace irx

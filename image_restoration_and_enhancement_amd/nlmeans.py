@@ -1,0 +1,95 @@
+"""Fast non-local means on the GPU: cv2.fastNlMeansDenoising / fastNlMeansDenoisingColored as the reference's
+classical denoise fallback calls them (`src/inference.py:509-515`, templateWindowSize 7, searchWindowSize 21),
+through `libirx.so` (csrc/nlmeans.hip, C ABI `irx_nlm_weights` / `irx_nlmeans_u8`).
+
+The invoker (integer patch distances, the weight table, the rounded integer average) is OpenCV's and exact
+against `oracle/nlm_ref.py`.  The colour conversion of the Colored variant (COLOR_LBGR2Lab and back, 8-bit
+Lab; the reference passes RGB bytes where cv2 expects BGR) runs on the host with `classical`'s restatement;
+cv2 is absent from this image, so parity against cv2 itself is unpinned.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+_LUT_CACHE: Dict[Tuple[float, int, int, int, str], torch.Tensor] = {}
+
+
+def nlm_weights(h: float, cn: int, template: int = 7, search: int = 21) -> np.ndarray:
+    """The invoker's weight table (almost_dist2weight), truncated at its first zero (host computation)."""
+    n = C.c_int()
+    L.call("irx_nlm_weights", float(h), cn, template, search, None, 0, C.byref(n))
+    buf = (C.c_int * max(n.value, 1))()
+    L.call("irx_nlm_weights", float(h), cn, template, search, buf, n.value, C.byref(n))
+    return np.frombuffer(buf, dtype=np.int32, count=n.value).copy()
+
+
+def _lut(h: float, cn: int, template: int, search: int, device) -> torch.Tensor:
+    key = (float(np.float32(h)), cn, template, search, str(device))
+    t = _LUT_CACHE.get(key)
+    if t is None:
+        t = torch.from_numpy(nlm_weights(h, cn, template, search)).to(device)
+        _LUT_CACHE[key] = t
+    return t
+
+
+def _check(img: torch.Tensor) -> torch.Tensor:
+    if img.dtype != torch.uint8 or not img.is_cuda:
+        raise ValueError("expected a uint8 CUDA tensor [H, W, C] or [B, H, W, C]")
+    return img.contiguous()
+
+
+def denoise_group(src: torch.Tensor, dst: torch.Tensor, h: float, ch_off: int, cn: int, template: int = 7,
+                  search: int = 21) -> None:
+    """Denoise channels [ch_off, ch_off + cn) of `src` into the same channels of `dst` ([B, H, W, C] uint8)."""
+    B, H, W, Cc = src.shape
+    lut = _lut(h, cn, template, search, src.device)
+    L.call("irx_nlmeans_u8", C.c_void_p(torch.cuda.current_stream().cuda_stream), C.c_void_p(src.data_ptr()),
+           C.c_void_p(dst.data_ptr()), B, H, W, Cc, ch_off, cn, template, search, C.c_void_p(lut.data_ptr()),
+           int(lut.numel()))
+
+
+def fast_nl_means_denoising(src: torch.Tensor, h: float = 3.0, template_window_size: int = 7,
+                            search_window_size: int = 21) -> torch.Tensor:
+    """cv2.fastNlMeansDenoising on uint8 images with 1 or 2 channels (one h for the channel group)."""
+    x = _check(src)
+    single = x.dim() == 3
+    if single:
+        x = x.unsqueeze(0)
+    if x.shape[-1] not in (1, 2):
+        raise ValueError("fastNlMeansDenoising: 1 or 2 channels (colour images: fast_nl_means_denoising_colored)")
+    out = torch.empty_like(x)
+    denoise_group(x, out, h, 0, x.shape[-1], template_window_size, search_window_size)
+    return out[0] if single else out
+
+
+def fast_nl_means_denoising_lab(lab: torch.Tensor, h: float, h_color: float, template_window_size: int = 7,
+                                search_window_size: int = 21) -> torch.Tensor:
+    """The invoker half of cv2.fastNlMeansDenoisingColored on 8-bit Lab images [B, H, W, 3]: L with `h`, the
+    (a, b) pair with `h_color` (denoising.cpp: mixChannels into l / ab, two fastNlMeansDenoising calls)."""
+    x = _check(lab)
+    if x.dim() != 4 or x.shape[-1] != 3:
+        raise ValueError("expected Lab images [B, H, W, 3]")
+    out = torch.empty_like(x)
+    denoise_group(x, out, h, 0, 1, template_window_size, search_window_size)
+    denoise_group(x, out, h_color, 1, 2, template_window_size, search_window_size)
+    return out
+
+
+def fast_nl_means_denoising_colored(img: np.ndarray, h: float = 3.0, h_color: float = 3.0,
+                                    template_window_size: int = 7, search_window_size: int = 21,
+                                    device: str = "cuda") -> np.ndarray:
+    """cv2.fastNlMeansDenoisingColored(img, None, h, hColor, 7, 21) for a uint8 [H, W, 3] (or [B, H, W, 3])
+    array: Lab conversion on the host, both invoker passes on the GPU."""
+    from . import classical
+    a = np.asarray(img, dtype=np.uint8)
+    lab = classical.lbgr_to_lab_u8(a)
+    dev = torch.from_numpy(np.ascontiguousarray(lab if lab.ndim == 4 else lab[None])).to(device)
+    out = fast_nl_means_denoising_lab(dev, h, h_color, template_window_size, search_window_size).cpu().numpy()
+    rgb = classical.lab_u8_to_lbgr(out)
+    return rgb if a.ndim == 4 else rgb[0]

@@ -158,6 +158,17 @@ int irx_degrade_gray(void* stream, const uint8_t* img, long npix, int mode, int 
 int irx_degrade_strokes(void* stream, int batch, int H, int W, const int* segs, const int* thick, const int* seg_off,
                         uint8_t* mask, const uint8_t* img, uint8_t* masked);
 
+/* ---- fast non-local means (cv2.fastNlMeansDenoising / ...Colored as src/inference.py:509-515 calls them in the
+ * classical denoise fallback _denoise_opencv :500-522).  OpenCV's integer invoker, exact. ---- */
+/* Host only: the invoker's weight table (almost_dist2weight) for filter strength h over `cn`-channel groups,
+ * truncated at its first zero; writes *lut_len and, if `lut`, the entries (cap = capacity of lut). */
+int irx_nlm_weights(float h, int cn, int template_size, int search_size, int* lut, int cap, int* lut_len);
+/* Denoise one channel group (cn = 1 or 2 channels starting at ch_off) of uint8 [batch][H][W][pix_stride] images
+ * from src into the same channels of dst (src != dst); lut = device copy of irx_nlm_weights' table.
+ * (template, search) in {(7, 21), (3, 5)}. */
+int irx_nlmeans_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int pix_stride,
+                   int ch_off, int cn, int template_size, int search_size, const int* lut, int lut_len);
+
 /* ---- single-op entry points (parity tests, composition) ---- */
 int irx_op_conv2d(void* stream, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hin, int win,
                   int hv, int wv, const void* weight, const float* bias, int cout, int kh, int kw, int stride,

@@ -1,0 +1,48 @@
+"""Fast NLM host checks: the oracle's two forms agree, the product CPU form and the C-ABI
+weight table match the oracle exactly, the colour wrapper's channel handling.  No GPU calls."""
+import numpy as np
+import pytest
+
+from image_restoration_and_enhancement_amd import classical as CL
+from oracle import nlm_ref as R
+
+
+@pytest.mark.parametrize("shape,h,t,s", [((6, 5, 2), 20.0, 3, 5), ((9, 11, 1), 10.0, 5, 7), ((4, 3, 1), 3.0, 3, 5),
+                                         ((1, 7, 2), 5.0, 3, 5)])
+def test_oracle_vectorised_matches_loop_form(shape, h, t, s):
+    img = np.random.default_rng(sum(shape)).integers(0, 256, shape, dtype=np.uint8)
+    assert np.array_equal(R.nl_means_u8(img, h, t, s), R.nl_means_u8_naive(img, h, t, s))
+
+
+def test_oracle_weight_table_anchors():
+    lut = R.weight_lut(20.0, 2)
+    assert R.bin_shift(7) == 6 and lut[0] == (2 ** 31 - 1) // (21 * 21 * 255) == 19096
+    assert len(lut) == int(255 * 255 * 2 * 49 / 64 + 1)
+    assert np.all(np.diff(lut) <= 0) and lut[-1] == 0
+    lut0 = R.weight_lut(0.0, 1)                       # h = 0: NaN at distance 0 -> 1, else 0
+    assert lut0[0] == 19096 and not lut0[1:].any()
+
+
+@pytest.mark.parametrize("h,cn", [(20.0, 1), (20.0, 2), (5.0, 1), (3.0000000000000004, 2), (0.0, 1), (37.5, 2)])
+def test_cabi_weight_table_matches_oracle(h, cn):
+    from image_restoration_and_enhancement_amd import nlmeans
+    ref = R.weight_lut(h, cn)
+    n = int((ref > 0).sum())
+    assert np.array_equal(nlmeans.nlm_weights(h, cn), ref[:n])
+    assert np.array_equal(CL.nlm_weights(h, cn), ref)
+
+
+@pytest.mark.parametrize("cn,h", [(1, 10.0), (2, 20.0)])
+def test_classical_cpu_form_matches_oracle(cn, h):
+    img = np.random.default_rng(cn).integers(0, 256, (33, 40, cn), dtype=np.uint8)
+    assert np.array_equal(CL.nl_means_u8(img, h), R.nl_means_u8(img, h))
+
+
+def test_colored_groups_and_channel_order():
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (20, 18, 3), dtype=np.uint8)
+    lab = CL.lbgr_to_lab_u8(img)
+    assert np.array_equal(lab, CL.rgb_to_lab_u8(img[..., ::-1], srgb=False))
+    out = CL.fast_nl_means_denoising_colored(img, 10.0, 15.0, 3, 5)
+    exp_lab = np.concatenate([R.nl_means_u8(lab[..., :1], 10.0, 3, 5), R.nl_means_u8(lab[..., 1:], 15.0, 3, 5)], -1)
+    assert np.array_equal(out, CL.lab_u8_to_lbgr(exp_lab))

@@ -162,9 +162,9 @@ def test_median_and_bilateral_shapes():
 
 def test_nl_means_reduces_noise():
     rng = np.random.default_rng(2)
-    clean = np.full((24, 24, 3), 120.0)
-    noisy = clean + rng.normal(0, 8, clean.shape)
-    out = CL.nl_means(noisy, np.array([10.0, 10.0, 10.0]), 7, 11)
+    clean = np.full((24, 24, 1), 120.0)
+    noisy = np.clip(np.rint(clean + rng.normal(0, 8, clean.shape)), 0, 255).astype(np.uint8)
+    out = CL.nl_means_u8(noisy, 10.0, 7, 11)
     assert np.abs(out - clean).mean() < 0.5 * np.abs(noisy - clean).mean()
 
 
