@@ -23,7 +23,8 @@ ARCH = os.environ.get("IRX_OFFLOAD_ARCH", "gfx950")
 BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
               "-Wno-unused-variable", "-Wno-unused-but-set-variable", f"-I{INCLUDE}"]
 PER_FILE = {"elementwise.hip": ["-ffp-contract=off"],
-            "attention.hip": ["-fno-honor-nans"]}   # fmaxf without NaN-quieting canonicalisations
+            "attention.hip": ["-fno-honor-nans"],
+            "filters.hip": ["-ffp-contract=off"]}   # fmaxf without NaN-quieting canonicalisations
 
 
 def _hipcc() -> str:

@@ -147,26 +147,30 @@ def fast_nl_means_denoising_colored(img: np.ndarray, h: float, h_color: float, t
 
 
 def bilateral(img: np.ndarray, d: int = 9, sigma_color: float = 75.0, sigma_space: float = 75.0) -> np.ndarray:
-    """cv2.bilateralFilter for uint8 RGB: circular window of radius d//2, colour distance = sum of
-    per-channel absolute differences, reflect-101 borders."""
-    r = d // 2
-    x = img.astype(np.float64)
-    H, W, _ = x.shape
-    pad = np.pad(x, ((r, r), (r, r), (0, 0)), mode="reflect")
-    gc, gs = -0.5 / sigma_color ** 2, -0.5 / sigma_space ** 2
-    acc = np.zeros_like(x)
-    wsum = np.zeros((H, W))
+    """cv2.bilateralFilter for uint8 images (BilateralFilter_8u): circular window of radius d//2 in row-major
+    order, colour distance = sum of per-channel absolute differences, fp32 tables and sums (one rounding per
+    operation, as csrc/filters.hip), cvRound(sum * (1 / wsum)), reflect-101 borders."""
+    H, W, cn = img.shape
+    sigma_color = 1.0 if sigma_color <= 0 else sigma_color
+    sigma_space = 1.0 if sigma_space <= 0 else sigma_space
+    r = max(d // 2 if d > 0 else int(np.rint(sigma_space * 1.5)), 1)
+    i = np.arange(256 * cn, dtype=np.float64)
+    cw = np.exp(i * i * (-0.5 / sigma_color ** 2)).astype(np.float32)
+    pad = np.pad(img, ((r, r), (r, r), (0, 0)), mode="reflect").astype(np.int64)
+    ctr = pad[r:r + H, r:r + W]
+    acc = np.zeros((H, W, cn), np.float32)
+    wsum = np.zeros((H, W), np.float32)
     for dy in range(-r, r + 1):
         for dx in range(-r, r + 1):
-            rr = np.sqrt(dy * dy + dx * dx)
+            rr = np.sqrt(float(dy * dy) + float(dx * dx))
             if rr > r:
                 continue
+            sw = np.float32(np.exp(rr * rr * (-0.5 / sigma_space ** 2)))
             sh = pad[r + dy:r + dy + H, r + dx:r + dx + W]
-            cd = np.abs(sh - x).sum(-1)
-            w = np.exp(rr * rr * gs + cd * cd * gc)
-            acc += w[..., None] * sh
-            wsum += w
-    return np.clip(np.rint(acc / wsum[..., None]), 0, 255).astype(np.uint8)
+            w = sw * cw[np.abs(sh - ctr).sum(-1)]
+            wsum = wsum + w
+            acc = acc + sh.astype(np.float32) * w[..., None]
+    return np.clip(np.rint(acc * (np.float32(1.0) / wsum)[..., None]), 0, 255).astype(np.uint8)
 
 
 def median5(img: np.ndarray) -> np.ndarray:
@@ -175,18 +179,19 @@ def median5(img: np.ndarray) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------------------- tasks
-def denoise_opencv(image: Image.Image, strength: float, nlm=None) -> Image.Image:
-    """src/inference.py:500-522.  `nlm` = the fastNlMeansDenoisingColored implementation (the GPU one from
-    `nlmeans` on a ROCm device; this module's numpy form otherwise)."""
+def denoise_opencv(image: Image.Image, strength: float, nlm=None, bilateral_fn=None, median_fn=None) -> Image.Image:
+    """src/inference.py:500-522.  `nlm` / `bilateral_fn` / `median_fn` = the fastNlMeansDenoisingColored,
+    bilateralFilter(9, 75, 75) and medianBlur(5) implementations (the GPU ones from `nlmeans` on a ROCm device;
+    this module's numpy forms otherwise)."""
     img = np.array(image.convert("RGB"))
     hs = float(np.clip(strength, 0.1, 1.0))
     h_value = hs * 10 if hs < 0.6 else 20          # luminance strength
     h_color = hs * 10 if hs < 0.6 else 20          # chroma strength (same rule in the reference)
     den = (nlm or fast_nl_means_denoising_colored)(img, h_value, h_color, 7, 21)
     if strength > 0.6:
-        den = bilateral(den, 9, 75, 75)
+        den = (bilateral_fn or bilateral)(den, 9, 75, 75)
     if strength > 0.8:
-        den = median5(den)
+        den = (median_fn or median5)(den)
     return Image.fromarray(den)
 
 

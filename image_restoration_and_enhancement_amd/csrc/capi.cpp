@@ -348,6 +348,52 @@ int irx_nlmeans_u8(void* s, const uint8_t* src, uint8_t* dst, int batch, int H, 
   IRX_API_END
 }
 
+// ------------------------------------------------------------------ bilateral / median filters
+int irx_bilateral_tables(int d, double sigma_color, double sigma_space, int cn, float* color_w, float* space_w,
+                         int* space_dydx, int cap, int* maxk, int* radius) {
+  IRX_API_BEGIN
+  IRX_CHECK(maxk && radius && cn >= 1 && cn <= 4, "bad arguments");
+  // bilateralFilter_8u (OpenCV 4.x): sigma <= 0 -> 1; radius d/2 (or cvRound(1.5 sigma_space) if d <= 0), >= 1
+  if (sigma_color <= 0) sigma_color = 1;
+  if (sigma_space <= 0) sigma_space = 1;
+  const double gc = -0.5 / (sigma_color * sigma_color), gs = -0.5 / (sigma_space * sigma_space);
+  int r = d <= 0 ? (int)std::nearbyint(sigma_space * 1.5) : d / 2;
+  r = std::max(r, 1);
+  if (color_w)
+    for (int i = 0; i < 256 * cn; ++i) color_w[i] = (float)std::exp(i * i * gc);
+  int k = 0;
+  for (int i = -r; i <= r; ++i)
+    for (int j = -r; j <= r; ++j) {
+      const double rr = std::sqrt((double)i * i + (double)j * j);
+      if (rr > r) continue;
+      if (space_w) {
+        IRX_CHECK(k < cap, "space table capacity too small");
+        space_w[k] = (float)std::exp(rr * rr * gs);
+        space_dydx[2 * k] = i;
+        space_dydx[2 * k + 1] = j;
+      }
+      ++k;
+    }
+  *maxk = k;
+  *radius = r;
+  IRX_API_END
+}
+int irx_bilateral_u8(void* s, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int radius,
+                     const float* space_w, const int* space_dydx, int maxk, const float* color_w) {
+  IRX_API_BEGIN
+  IRX_CHECK(src && dst && src != dst && space_w && space_dydx && color_w && batch >= 0 && H > 0 && W > 0,
+            "bad arguments");
+  if (batch) bilateral_u8(src, dst, batch, H, W, radius, space_w, space_dydx, maxk, color_w, S(s));
+  IRX_API_END
+}
+int irx_median_blur_u8(void* s, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int C, int ksize) {
+  IRX_API_BEGIN
+  IRX_CHECK(src && dst && src != dst && batch >= 0 && H > 0 && W > 0, "bad arguments");
+  IRX_CHECK(ksize == 5, "medianBlur: compiled for ksize 5");
+  if (batch) median5_u8(src, dst, batch, H, W, C, S(s));
+  IRX_API_END
+}
+
 // ------------------------------------------------------------------ single ops
 int irx_op_conv2d(void* s, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hin, int win, int hv,
                   int wv, const void* weight, const float* bias, int cout, int kh, int kw, int stride, int pad_t,

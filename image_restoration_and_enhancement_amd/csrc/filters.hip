@@ -1,0 +1,124 @@
+// irx — the two edge-preserving filters that follow the NLM pass in the reference's classical denoise fallback
+// (src/inference.py:517-520), on uint8 [B][H][W][3] batches resident in HBM:
+//   * bilateral_kernel  cv2.bilateralFilter(img, 9, 75, 75) for 8-bit 3-channel images (BilateralFilter_8u):
+//     circular window (offsets with sqrt(i^2 + j^2) <= r, row-major), w = space_w[k] * color_w[|db|+|dg|+|dr|]
+//     in fp32 from host-built tables, per-pixel sums accumulated in window order without contraction, result
+//     cvRound(sum * (1 / wsum)); BORDER_REFLECT_101.  Checked bit-exact against oracle/filters_ref.py.
+//   * median_kernel     cv2.medianBlur(img, 5): per-channel 5x5 median, BORDER_REPLICATE (exact).
+// Both stage a reflect/replicate-padded tile in LDS and are VALU-bound: HBM traffic is one read and one write.
+#include "ops.h"
+#include "profile.h"
+
+namespace irx {
+namespace {
+
+constexpr int FT_W = 32, FT_H = 8;                            // 32x8 pixel tile, one pixel per thread
+
+__device__ __forceinline__ int refl101f(int p, int n) {
+  if (n == 1) return 0;
+  while ((unsigned)p >= (unsigned)n) p = p < 0 ? -p : 2 * (n - 1) - p;
+  return p;
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void bilateral_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                        int H, int W, const float* __restrict__ space_w,
+                                                        const int* __restrict__ space_dydx, int maxk,
+                                                        const float* __restrict__ color_w) {
+  constexpr int RH = FT_H + 2 * R, RW = FT_W + 2 * R;
+  __shared__ uint32_t tile[RH * RW];                          // packed b | g << 8 | r << 16
+  __shared__ float cw[256 * 3];
+  __shared__ float sw[(2 * R + 1) * (2 * R + 1)];
+  __shared__ int so[(2 * R + 1) * (2 * R + 1)];
+  const int tid = threadIdx.x, x0 = blockIdx.x * FT_W, y0 = blockIdx.y * FT_H;
+  const uint8_t* img = src + (size_t)blockIdx.z * H * W * 3;
+  for (int i = tid; i < RH * RW; i += 256) {
+    const int ry = i / RW, rx = i - ry * RW;
+    const uint8_t* p = img + ((size_t)refl101f(y0 + ry - R, H) * W + refl101f(x0 + rx - R, W)) * 3;
+    tile[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+  }
+  for (int i = tid; i < 256 * 3; i += 256) cw[i] = color_w[i];
+  for (int i = tid; i < maxk; i += 256) {
+    sw[i] = space_w[i];
+    so[i] = (space_dydx[2 * i] + R) * RW + space_dydx[2 * i + 1] + R;   // tile offset of (dy, dx)
+  }
+  __syncthreads();
+  const int tx = tid % FT_W, ty = tid / FT_W, x = x0 + tx, y = y0 + ty;
+  const uint32_t* base = tile + ty * RW + tx;
+  const uint32_t c0 = base[R * RW + R];
+  const int b0 = c0 & 255, g0 = (c0 >> 8) & 255, r0 = c0 >> 16;
+  float wsum = 0.f, sb = 0.f, sg = 0.f, sr = 0.f;
+  for (int k = 0; k < maxk; ++k) {
+    const uint32_t c = base[so[k]];
+    const int b = c & 255, g = (c >> 8) & 255, r = c >> 16;
+    const float w = __fmul_rn(sw[k], cw[abs(b - b0) + abs(g - g0) + abs(r - r0)]);
+    wsum = __fadd_rn(wsum, w);
+    sb = __fadd_rn(sb, __fmul_rn((float)b, w));
+    sg = __fadd_rn(sg, __fmul_rn((float)g, w));
+    sr = __fadd_rn(sr, __fmul_rn((float)r, w));
+  }
+  if (y < H && x < W) {
+    const float inv = __fdiv_rn(1.f, wsum);
+    uint8_t* o = dst + (((size_t)blockIdx.z * H + y) * W + x) * 3;
+    o[0] = (uint8_t)min(255, max(0, (int)rintf(__fmul_rn(sb, inv))));
+    o[1] = (uint8_t)min(255, max(0, (int)rintf(__fmul_rn(sg, inv))));
+    o[2] = (uint8_t)min(255, max(0, (int)rintf(__fmul_rn(sr, inv))));
+  }
+}
+
+__global__ __launch_bounds__(256) void median_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                     int H, int W, int C) {
+  constexpr int R = 2, RH = FT_H + 2 * R, RW = FT_W + 2 * R;
+  __shared__ uint8_t tile[4][RH * RW];
+  const int tid = threadIdx.x, x0 = blockIdx.x * FT_W, y0 = blockIdx.y * FT_H;
+  const uint8_t* img = src + (size_t)blockIdx.z * H * W * C;
+  for (int i = tid; i < RH * RW; i += 256) {
+    const int ry = i / RW, rx = i - ry * RW;
+    const int gy = min(max(y0 + ry - R, 0), H - 1), gx = min(max(x0 + rx - R, 0), W - 1);
+    for (int c = 0; c < C; ++c) tile[c][i] = img[((size_t)gy * W + gx) * C + c];
+  }
+  __syncthreads();
+  const int tx = tid % FT_W, ty = tid / FT_W, x = x0 + tx, y = y0 + ty;
+  if (y >= H || x >= W) return;
+  for (int c = 0; c < C; ++c) {
+    int v[25];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) v[i * 5 + j] = tile[c][(ty + i) * RW + tx + j];
+    // the 13th smallest: the value with < 13 smaller and >= 13 smaller-or-equal elements
+    int med = 0;
+#pragma unroll
+    for (int i = 0; i < 25; ++i) {
+      int lt = 0, le = 0;
+#pragma unroll
+      for (int j = 0; j < 25; ++j) {
+        lt += v[j] < v[i];
+        le += v[j] <= v[i];
+      }
+      med = (lt <= 12 && le >= 13) ? v[i] : med;
+    }
+    dst[(((size_t)blockIdx.z * H + y) * W + x) * C + c] = (uint8_t)med;
+  }
+}
+
+}  // namespace
+
+void bilateral_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int radius, const float* space_w,
+                  const int* space_dydx, int maxk, const float* color_w, hipStream_t s) {
+  IRX_CHECK(radius == 4 && maxk >= 1 && maxk <= 81, "bilateral: compiled for d = 9 (radius 4)");
+  const dim3 grid((W + FT_W - 1) / FT_W, (H + FT_H - 1) / FT_H, N);
+  ProfScope pr(prof_on() ? std::string("irx::(anonymous namespace)::bilateral_kernel") : std::string(), 0.0, s);
+  hipLaunchKernelGGL(bilateral_kernel<4>, grid, dim3(256), 0, s, src, dst, H, W, space_w, space_dydx, maxk, color_w);
+  IRX_HIP(hipGetLastError());
+}
+
+void median5_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int C, hipStream_t s) {
+  IRX_CHECK(C >= 1 && C <= 4, "median: 1 to 4 channels");
+  const dim3 grid((W + FT_W - 1) / FT_W, (H + FT_H - 1) / FT_H, N);
+  ProfScope pr(prof_on() ? std::string("irx::(anonymous namespace)::median_kernel") : std::string(), 0.0, s);
+  hipLaunchKernelGGL(median_kernel, grid, dim3(256), 0, s, src, dst, H, W, C);
+  IRX_HIP(hipGetLastError());
+}
+
+}  // namespace irx

@@ -150,5 +150,9 @@ void degrade_strokes(int B, int H, int W, const int* segs, const int* thick, con
 // ------------------------------------------------------------ fast non-local means (nlmeans.hip)
 void nlmeans_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, int cn, int tmpl,
                 int search, const int* lut, int lut_len, int shift, hipStream_t s);
+// ------------------------------------------------------------ bilateral / median (filters.hip)
+void bilateral_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int radius, const float* space_w,
+                  const int* space_dydx, int maxk, const float* color_w, hipStream_t s);
+void median5_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int C, hipStream_t s);
 
 }  // namespace irx

@@ -262,9 +262,9 @@ class RestorationPipeline:
             return self._denoise_opencv(image, strength=strength)
 
     def _denoise_opencv(self, image: Image.Image, strength: float) -> Image.Image:
-        if self.device.startswith("cuda"):         # NLM invoker on the GPU (csrc/nlmeans.hip); no CPU retry
+        if self.device.startswith("cuda"):         # NLM + bilateral + median on the GPU; no CPU retry
             from . import nlmeans
-            return classical.denoise_opencv(image, strength, nlm=nlmeans.fast_nl_means_denoising_colored)
+            return nlmeans.denoise_opencv(image, strength, device=self.device)
         return classical.denoise_opencv(image, strength)
 
     # ------------------------------------------------------------------------------------ super-resolution

@@ -1,6 +1,7 @@
-"""Fast non-local means on the GPU: cv2.fastNlMeansDenoising / fastNlMeansDenoisingColored as the reference's
-classical denoise fallback calls them (`src/inference.py:509-515`, templateWindowSize 7, searchWindowSize 21),
-through `libirx.so` (csrc/nlmeans.hip, C ABI `irx_nlm_weights` / `irx_nlmeans_u8`).
+"""The reference's classical denoise fallback (`src/inference.py:500-522`) on the GPU: cv2.fastNlMeansDenoising /
+fastNlMeansDenoisingColored (templateWindowSize 7, searchWindowSize 21; csrc/nlmeans.hip, C ABI `irx_nlm_weights`
+/ `irx_nlmeans_u8`), cv2.bilateralFilter(9, 75, 75) and cv2.medianBlur(5) (csrc/filters.hip,
+`irx_bilateral_tables` / `irx_bilateral_u8` / `irx_median_blur_u8`), and `denoise_opencv` composing them.
 
 The invoker (integer patch distances, the weight table, the rounded integer average) is OpenCV's and exact
 against `oracle/nlm_ref.py`.  The colour conversion of the Colored variant (COLOR_LBGR2Lab and back, 8-bit
@@ -93,3 +94,69 @@ def fast_nl_means_denoising_colored(img: np.ndarray, h: float = 3.0, h_color: fl
     out = fast_nl_means_denoising_lab(dev, h, h_color, template_window_size, search_window_size).cpu().numpy()
     rgb = classical.lab_u8_to_lbgr(out)
     return rgb if a.ndim == 4 else rgb[0]
+
+
+_BIL_CACHE: Dict[Tuple[int, float, float, str], tuple] = {}
+
+
+def _bilateral_tables(d: int, sigma_color: float, sigma_space: float, device):
+    key = (d, float(sigma_color), float(sigma_space), str(device))
+    t = _BIL_CACHE.get(key)
+    if t is None:
+        maxk, radius = C.c_int(), C.c_int()
+        L.call("irx_bilateral_tables", d, float(sigma_color), float(sigma_space), 3, None, None, None, 0,
+               C.byref(maxk), C.byref(radius))
+        cw = np.zeros(256 * 3, np.float32)
+        sw = np.zeros(maxk.value, np.float32)
+        dydx = np.zeros(2 * maxk.value, np.int32)
+        L.call("irx_bilateral_tables", d, float(sigma_color), float(sigma_space), 3, C.c_void_p(cw.ctypes.data),
+               C.c_void_p(sw.ctypes.data), C.c_void_p(dydx.ctypes.data), maxk.value, C.byref(maxk), C.byref(radius))
+        t = (torch.from_numpy(cw).to(device), torch.from_numpy(sw).to(device), torch.from_numpy(dydx).to(device),
+             maxk.value, radius.value)
+        _BIL_CACHE[key] = t
+    return t
+
+
+def bilateral_filter(src: torch.Tensor, d: int = 9, sigma_color: float = 75.0, sigma_space: float = 75.0
+                     ) -> torch.Tensor:
+    """cv2.bilateralFilter on uint8 RGB/BGR images [H, W, 3] or [B, H, W, 3] (d = 9)."""
+    x = _check(src)
+    single = x.dim() == 3
+    if single:
+        x = x.unsqueeze(0)
+    if x.shape[-1] != 3:
+        raise ValueError("bilateralFilter: 3-channel images")
+    cw, sw, dydx, maxk, radius = _bilateral_tables(d, sigma_color, sigma_space, x.device)
+    out = torch.empty_like(x)
+    B, H, W, _ = x.shape
+    L.call("irx_bilateral_u8", C.c_void_p(torch.cuda.current_stream().cuda_stream), C.c_void_p(x.data_ptr()),
+           C.c_void_p(out.data_ptr()), B, H, W, radius, C.c_void_p(sw.data_ptr()), C.c_void_p(dydx.data_ptr()),
+           maxk, C.c_void_p(cw.data_ptr()))
+    return out[0] if single else out
+
+
+def median_blur(src: torch.Tensor, ksize: int = 5) -> torch.Tensor:
+    """cv2.medianBlur(img, 5) on uint8 images [H, W, C] or [B, H, W, C], C <= 4."""
+    x = _check(src)
+    single = x.dim() == 3
+    if single:
+        x = x.unsqueeze(0)
+    out = torch.empty_like(x)
+    B, H, W, Cc = x.shape
+    L.call("irx_median_blur_u8", C.c_void_p(torch.cuda.current_stream().cuda_stream), C.c_void_p(x.data_ptr()),
+           C.c_void_p(out.data_ptr()), B, H, W, Cc, ksize)
+    return out[0] if single else out
+
+
+def denoise_opencv(image, strength: float, device: str = "cuda"):
+    """RestorationPipeline._denoise_opencv (src/inference.py:500-522) with every filter on the GPU."""
+    from . import classical
+
+    def bil(a, d, sc, ss):
+        return bilateral_filter(torch.from_numpy(np.ascontiguousarray(a)).to(device), d, sc, ss).cpu().numpy()
+
+    def med(a):
+        return median_blur(torch.from_numpy(np.ascontiguousarray(a)).to(device), 5).cpu().numpy()
+
+    return classical.denoise_opencv(image, strength, nlm=lambda *a: fast_nl_means_denoising_colored(*a, device=device),
+                                    bilateral_fn=bil, median_fn=med)

@@ -169,6 +169,18 @@ int irx_nlm_weights(float h, int cn, int template_size, int search_size, int* lu
 int irx_nlmeans_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int pix_stride,
                    int ch_off, int cn, int template_size, int search_size, const int* lut, int lut_len);
 
+/* ---- the filters after the NLM pass in _denoise_opencv (src/inference.py:517-520) ---- */
+/* Host only: cv2.bilateralFilter's tables (BilateralFilter_8u): color_w[256*cn] = f32(exp(-i^2 / 2sc^2)), and for
+ * the circular window (row-major, sqrt(i^2+j^2) <= radius) space_w[k] = f32(exp(-r^2 / 2ss^2)), space_dydx[2k] =
+ * (i, j).  Null table pointers: sizes only.  Writes *maxk and *radius. */
+int irx_bilateral_tables(int d, double sigma_color, double sigma_space, int cn, float* color_w, float* space_w,
+                         int* space_dydx, int cap, int* maxk, int* radius);
+/* cv2.bilateralFilter(img, d = 9, ...) on uint8 [batch][H][W][3] (src != dst), tables in device memory. */
+int irx_bilateral_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int radius,
+                     const float* space_w, const int* space_dydx, int maxk, const float* color_w);
+/* cv2.medianBlur(img, 5) on uint8 [batch][H][W][C], C <= 4 (src != dst). */
+int irx_median_blur_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int C, int ksize);
+
 /* ---- single-op entry points (parity tests, composition) ---- */
 int irx_op_conv2d(void* stream, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hin, int win,
                   int hv, int wv, const void* weight, const float* bias, int cout, int kh, int kw, int stride,

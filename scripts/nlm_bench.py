@@ -51,6 +51,17 @@ res = {"metric": "fastNlMeansDenoisingColored 7/21, images/s", "value": round(a.
        "direct_taps_per_s_T": round(pix * 441 * 49 * 3 / (ms / 1e3) / 1e12, 3),
        "hbm_bytes_per_batch": 2 * pix * 3 * 2,
        "kernels": [(n, c, round(t / max(c, 1) * 1e3, 1)) for n, c, t, _ in prof]}
+rgb = lab
+for name, fn in (("bilateral_9_75_75", lambda: N.bilateral_filter(rgb, 9, 75, 75)),
+                 ("median_5", lambda: N.median_blur(rgb, 5))):
+    fn()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(a.iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    res[name + "_ms_per_batch"] = round(e0.elapsed_time(e1) / a.iters, 3)
 if a.cpu:
     t = time.time()
     img = noisy[0]

@@ -80,3 +80,28 @@ def test_nlm_rejects_unsupported_windows_and_aliasing(device):
         N.denoise_group(x, x, 10.0, 0, 1)
     with pytest.raises(ValueError):
         N.fast_nl_means_denoising(torch.zeros((16, 16, 3), dtype=torch.uint8, device=device), 10.0)
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (3, 5), (8, 32), (37, 70), (130, 97)])
+def test_bilateral_bit_exact(device, shape):
+    from oracle import filters_ref as F
+    img = _img((2, *shape, 3), seed=shape[1])
+    got = N.bilateral_filter(torch.from_numpy(img).to(device), 9, 75, 75).cpu().numpy()
+    for b in range(2):
+        assert np.array_equal(got[b], F.bilateral_u8(img[b], 9, 75, 75)), b
+
+
+def test_bilateral_other_sigmas(device):
+    from oracle import filters_ref as F
+    img = _img((64, 48, 3), seed=4)
+    got = N.bilateral_filter(torch.from_numpy(img).to(device), 9, 20.0, 3.0).cpu().numpy()
+    assert np.array_equal(got, F.bilateral_u8(img, 9, 20.0, 3.0))
+
+
+@pytest.mark.parametrize("shape,c", [((1, 1), 3), ((4, 3), 1), ((33, 65), 3), ((40, 41), 4)])
+def test_median_exact(device, shape, c):
+    from oracle import filters_ref as F
+    img = _img((2, *shape, c), seed=c + shape[0])
+    got = N.median_blur(torch.from_numpy(img).to(device), 5).cpu().numpy()
+    for b in range(2):
+        assert np.array_equal(got[b], F.median5_u8(img[b])), b
