@@ -71,6 +71,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gemm_small") g_gemm_small = value != 0;
   else if (n == "attn_d40") g_attn_d40 = value;
   else if (n == "gemm_small_kmax") g_gemm_small_kmax = value;
+  else if (n == "nlm_strip") g_nlm_strip = value;
   else throw Error("unknown option " + n);
   IRX_API_END
 }

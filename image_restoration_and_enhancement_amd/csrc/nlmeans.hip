@@ -19,9 +19,10 @@
 #include <type_traits>
 
 namespace irx {
+int g_nlm_strip = 4;                               // irx_set_option("nlm_strip", 4 | 8)
 namespace {
 
-constexpr int NLM_TW = 32, NLM_S = 4, NLM_G = 8, NLM_TH = NLM_S * NLM_G;   // 32x32 tile, 256 threads
+constexpr int NLM_TW = 32, NLM_G = 8;          // 32 columns x 8 strip groups = 256 threads; strips of S rows
 
 __device__ __forceinline__ int refl101(int p, int n) {
   if (n == 1) return 0;
@@ -44,11 +45,12 @@ __device__ __forceinline__ int tap(int s, int o, int n) {
   }
 }
 
-template <int CN, int TR, int SR>
+template <int CN, int TR, int SR, int NLM_S>
 __global__ __launch_bounds__(256) void nlm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                   int H, int W, int ps, int coff, const int* __restrict__ lut,
                                                   int lut_len, int shift) {
   static_assert(CN == 1 || CN == 2, "channel groups of 1 or 2");
+  constexpr int NLM_TH = NLM_S * NLM_G;
   using PV = typename std::conditional<CN == 1, uint8_t, uint32_t>::type;
   constexpr int B = TR + SR, T = 2 * TR + 1, RH = NLM_TH + 2 * B, RW = NLM_TW + 2 * B, NR = NLM_S + 2 * TR;
   constexpr int PLANE = RH * RW;
@@ -135,13 +137,14 @@ __global__ __launch_bounds__(256) void nlm_kernel(const uint8_t* __restrict__ sr
   }
 }
 
-template <int CN, int TR, int SR>
+template <int CN, int TR, int SR, int NLM_S>
 void launch(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, const int* lut, int lut_len,
             int shift, hipStream_t s) {
-  constexpr int B = TR + SR, PLANE = (NLM_TH + 2 * B) * (NLM_TW + 2 * B), PB = CN == 1 ? 1 : 4;
+  constexpr int NLM_TH = NLM_S * NLM_G, B = TR + SR, PLANE = (NLM_TH + 2 * B) * (NLM_TW + 2 * B);
+  constexpr int PB = CN == 1 ? 1 : 4;
   const size_t lds = ((PLANE * PB + 3) / 4 + lut_len + 1) * sizeof(int);
   IRX_CHECK(lds <= 160 * 1024, "nlmeans: weight table too long for LDS (h too large)");
-  auto k = nlm_kernel<CN, TR, SR>;
+  auto k = nlm_kernel<CN, TR, SR, NLM_S>;
   if (lds > 64 * 1024) IRX_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                    (int)lds));
   const dim3 grid((W + NLM_TW - 1) / NLM_TW, (H + NLM_TH - 1) / NLM_TH, N);
@@ -156,12 +159,15 @@ void launch(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int c
 
 void nlmeans_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, int cn, int tmpl,
                 int search, const int* lut, int lut_len, int shift, hipStream_t s) {
+  const int strip = g_nlm_strip;                   // strip rows per thread for the 1-channel group (4 or 8)
   if (tmpl == 7 && search == 21) {
-    if (cn == 1) return launch<1, 3, 10>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
-    if (cn == 2) return launch<2, 3, 10>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+    if (cn == 1 && strip == 8) return launch<1, 3, 10, 8>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+    if (cn == 1) return launch<1, 3, 10, 4>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+    if (cn == 2) return launch<2, 3, 10, 4>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
   } else if (tmpl == 3 && search == 5) {
-    if (cn == 1) return launch<1, 1, 2>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
-    if (cn == 2) return launch<2, 1, 2>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+    if (cn == 1 && strip == 8) return launch<1, 1, 2, 8>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+    if (cn == 1) return launch<1, 1, 2, 4>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+    if (cn == 2) return launch<2, 1, 2, 4>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
   }
   IRX_CHECK(false, "nlmeans: supported (template, search, cn): (7, 21) and (3, 5) with cn 1 or 2");
 }

@@ -21,8 +21,11 @@ ap.add_argument("--batch", type=int, default=8)
 ap.add_argument("--size", type=int, default=512)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--cpu", action="store_true")
+ap.add_argument("--strip", type=int, default=0, help="irx option nlm_strip (0: library default)")
 a = ap.parse_args()
 
+if a.strip:
+    L.call("irx_set_option", b"nlm_strip", a.strip)
 rng = np.random.default_rng(0)
 y, x = np.mgrid[0:a.size, 0:a.size]
 clean = np.stack([(x + y) / 4, 128 + 40 * np.sin(x / 25.0), 128 + 40 * np.cos(y / 30.0)], -1)

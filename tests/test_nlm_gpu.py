@@ -105,3 +105,15 @@ def test_median_exact(device, shape, c):
     got = N.median_blur(torch.from_numpy(img).to(device), 5).cpu().numpy()
     for b in range(2):
         assert np.array_equal(got[b], F.median5_u8(img[b])), b
+
+
+@pytest.mark.parametrize("tmpl,search", [(3, 5), (7, 21)])
+def test_nlm_strip8_variant_bit_exact(device, tmpl, search):
+    img = _img((2, 45, 70, 1), seed=tmpl)
+    L.call("irx_set_option", b"nlm_strip", 8)
+    try:
+        got = N.fast_nl_means_denoising(torch.from_numpy(img).to(device), 12.0, tmpl, search).cpu().numpy()
+    finally:
+        L.call("irx_set_option", b"nlm_strip", 4)
+    for b in range(2):
+        assert np.array_equal(got[b], R.nl_means_u8(img[b], 12.0, tmpl, search)), b
