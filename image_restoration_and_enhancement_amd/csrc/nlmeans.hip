@@ -20,6 +20,7 @@
 
 namespace irx {
 int g_nlm_strip = 4;                               // irx_set_option("nlm_strip", 4 | 8)
+int g_nlm_v2 = 1;                                  // irx_set_option("nlm_v2", 0): v1 register-window kernel
 namespace {
 
 constexpr int NLM_TW = 32, NLM_G = 8;          // 32 columns x 8 strip groups = 256 threads; strips of S rows
@@ -137,6 +138,126 @@ __global__ __launch_bounds__(256) void nlm_kernel(const uint8_t* __restrict__ sr
   }
 }
 
+// v2: per search offset each lane squares only its own column, (S + 2r) taps for an S-row strip; the template
+// sums are a running vertical sum per lane and a 2r-step horizontal sum across lanes, each step one
+// v_add_u32_dpp wave_shr:1.  A wave spans 64 consecutive columns and yields 64 - 2r outputs (lane l holds
+// the window ending at column l, centred on column l - r).  Search offsets run dx-major so the neighbour
+// column slides down one row per dy (one LDS read per offset).
+constexpr int NLM2_WAVES = 4;
+
+template <int CN, int TR, int SR, int S>
+__global__ __launch_bounds__(256) void nlm2_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   int H, int W, int ps, int coff, const int* __restrict__ lut,
+                                                   int lut_len, int shift) {
+  static_assert(CN == 1 || CN == 2, "channel groups of 1 or 2");
+  using PV = typename std::conditional<CN == 1, uint8_t, uint32_t>::type;
+  constexpr int TWO = 64 - 2 * TR, TH = NLM2_WAVES * S, B = TR + SR, NR = S + 2 * TR;
+  constexpr int RH = TH + 2 * B, RW = 64 + 2 * SR, PLANE = RH * RW;
+  extern __shared__ int smem[];
+  PV* reg = reinterpret_cast<PV*>(smem);                      // [RH][RW], origin (y0 - B, x0 - B)
+  int* wl = smem + (PLANE * (int)sizeof(PV) + 3) / 4;
+  const int tid = threadIdx.x, x0 = blockIdx.x * TWO, y0 = blockIdx.y * TH;
+  const uint8_t* img = src + (size_t)blockIdx.z * H * W * ps + coff;
+  for (int i = tid; i < PLANE; i += 256) {
+    const int ry = i / RW, rx = i - ry * RW;
+    const uint8_t* p = img + ((size_t)refl101(y0 + ry - B, H) * W + refl101(x0 + rx - B, W)) * ps;
+    if constexpr (CN == 1) reg[i] = p[0];
+    else reg[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 16);
+  }
+  for (int i = tid; i <= lut_len; i += 256) wl[i] = i < lut_len ? lut[i] : 0;
+  __syncthreads();
+
+  const int l = tid & 63, w = tid >> 6;
+  // own column (image column x0 - TR + l), rows y0 + w*S - TR + j
+  int own[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) own[j] = (int)reg[(w * S + SR + j) * RW + l + SR];
+  // centre pixel of the output this lane holds: column x0 - 2TR + l (window [l - 2TR, l])
+  int wsum[S], est[S][CN];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    wsum[i] = 0;
+#pragma unroll
+    for (int c = 0; c < CN; ++c) est[i][c] = 0;
+  }
+  for (int b = 0; b <= 2 * SR; ++b) {                         // dx = b - SR
+    const PV* cb = reg + w * S * RW + l + b;                  // neighbour column, row offset a + j
+    int nb[NR];
+#pragma unroll
+    for (int j = 0; j < NR - 1; ++j) nb[j] = (int)cb[j * RW];
+    for (int a = 0; a <= 2 * SR; ++a) {                       // dy = a - SR
+      nb[NR - 1] = (int)cb[(a + NR - 1) * RW];
+      int D[NR];
+#pragma unroll
+      for (int j = 0; j < NR; ++j) D[j] = tap<CN>(0, own[j], nb[j]);
+      int V[S];
+      {
+        int v = 0;
+#pragma unroll
+        for (int t = 0; t < 2 * TR + 1; ++t) v += D[t];
+        V[0] = v;
+#pragma unroll
+        for (int i = 1; i < S; ++i) {
+          v += D[i + 2 * TR] - D[i - 1];
+          V[i] = v;
+        }
+      }
+      // the centre value q of each output: neighbour at the centre column (lane l - TR), row i + TR
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        int hs = V[i];
+#pragma unroll
+        for (int u = 0; u < 2 * TR; ++u) hs = V[i] + __builtin_amdgcn_update_dpp(0, hs, 0x138, 0xf, 0xf, false);
+        const int q = __builtin_amdgcn_update_dpp(0, nb[i + TR], 0x138, 0xf, 0xf, false);
+        // q is from lane l - 1; the centre needs lane l - TR: shift TR - 1 more times
+        int qc = q;
+#pragma unroll
+        for (int u = 1; u < TR; ++u) qc = __builtin_amdgcn_update_dpp(0, qc, 0x138, 0xf, 0xf, false);
+        const int wt = wl[min(hs >> shift, lut_len)];
+        wsum[i] += wt;
+        if constexpr (CN == 1) {
+          est[i][0] += wt * qc;
+        } else {
+          est[i][0] += wt * (qc & 0xffff);
+          est[i][1] += wt * (qc >> 16);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NR - 1; ++j) nb[j] = nb[j + 1];
+    }
+  }
+  const int x = x0 - TR + l - TR;                             // centre column of this lane's window
+  if (l >= 2 * TR && x < W) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const int y = y0 + w * S + i;
+      if (y < H) {
+        uint8_t* o = dst + (((size_t)blockIdx.z * H + y) * W + x) * ps + coff;
+        const unsigned ws = (unsigned)wsum[i];
+#pragma unroll
+        for (int c = 0; c < CN; ++c) o[c] = (uint8_t)min(255u, ((unsigned)est[i][c] + ws / 2) / ws);
+      }
+    }
+  }
+}
+
+template <int CN, int TR, int SR>
+void launch2(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, const int* lut, int lut_len,
+             int shift, hipStream_t s) {
+  constexpr int S = 8, TWO = 64 - 2 * TR, TH = NLM2_WAVES * S, B = TR + SR;
+  constexpr int PLANE = (TH + 2 * B) * (64 + 2 * SR), PB = CN == 1 ? 1 : 4;
+  const size_t lds = ((PLANE * PB + 3) / 4 + lut_len + 1) * sizeof(int);
+  IRX_CHECK(lds <= 160 * 1024, "nlmeans: weight table too long for LDS (h too large)");
+  auto k = nlm2_kernel<CN, TR, SR, S>;
+  if (lds > 64 * 1024) IRX_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)lds));
+  const dim3 grid((W + TWO - 1) / TWO, (H + TH - 1) / TH, N);
+  const double ops = 3.0 * N * H * W * (2 * SR + 1) * (2 * SR + 1) * (2 * TR + 1) * (2 * TR + 1) * CN;
+  ProfScope pr(prof_on() ? std::string("irx::(anonymous namespace)::nlm2_kernel") : std::string(), ops, s);
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, src, dst, H, W, ps, coff, lut, lut_len, shift);
+  IRX_HIP(hipGetLastError());
+}
+
 template <int CN, int TR, int SR, int NLM_S>
 void launch(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, const int* lut, int lut_len,
             int shift, hipStream_t s) {
@@ -160,6 +281,15 @@ void launch(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int c
 void nlmeans_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, int cn, int tmpl,
                 int search, const int* lut, int lut_len, int shift, hipStream_t s) {
   const int strip = g_nlm_strip;                   // strip rows per thread for the 1-channel group (4 or 8)
+  if (g_nlm_v2) {
+    if (tmpl == 7 && search == 21) {
+      if (cn == 1) return launch2<1, 3, 10>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+      if (cn == 2) return launch2<2, 3, 10>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+    } else if (tmpl == 3 && search == 5) {
+      if (cn == 1) return launch2<1, 1, 2>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+      if (cn == 2) return launch2<2, 1, 2>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+    }
+  }
   if (tmpl == 7 && search == 21) {
     if (cn == 1 && strip == 8) return launch<1, 3, 10, 8>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
     if (cn == 1) return launch<1, 3, 10, 4>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);

@@ -22,8 +22,11 @@ ap.add_argument("--size", type=int, default=512)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--cpu", action="store_true")
 ap.add_argument("--strip", type=int, default=0, help="irx option nlm_strip (0: library default)")
+ap.add_argument("--v2", type=int, default=-1, help="irx option nlm_v2 (-1: library default)")
 a = ap.parse_args()
 
+if a.v2 >= 0:
+    L.call("irx_set_option", b"nlm_v2", a.v2)
 if a.strip:
     L.call("irx_set_option", b"nlm_strip", a.strip)
 rng = np.random.default_rng(0)

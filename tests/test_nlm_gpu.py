@@ -110,10 +110,27 @@ def test_median_exact(device, shape, c):
 @pytest.mark.parametrize("tmpl,search", [(3, 5), (7, 21)])
 def test_nlm_strip8_variant_bit_exact(device, tmpl, search):
     img = _img((2, 45, 70, 1), seed=tmpl)
+    L.call("irx_set_option", b"nlm_v2", 0)
     L.call("irx_set_option", b"nlm_strip", 8)
     try:
         got = N.fast_nl_means_denoising(torch.from_numpy(img).to(device), 12.0, tmpl, search).cpu().numpy()
     finally:
         L.call("irx_set_option", b"nlm_strip", 4)
+        L.call("irx_set_option", b"nlm_v2", 1)
     for b in range(2):
         assert np.array_equal(got[b], R.nl_means_u8(img[b], 12.0, tmpl, search)), b
+
+
+@pytest.mark.parametrize("tmpl,search", [(3, 5), (7, 21)])
+@pytest.mark.parametrize("cn", [1, 2])
+@pytest.mark.parametrize("shape", [(1, 7), (13, 9), (37, 130), (70, 45)])
+def test_nlm_v1_register_window_bit_exact(device, tmpl, search, cn, shape):
+    """The v1 kernel (per-thread register window, irx option nlm_v2 = 0); the default v2 runs everywhere else."""
+    img = _img((2, *shape, cn), seed=tmpl + cn + shape[1])
+    L.call("irx_set_option", b"nlm_v2", 0)
+    try:
+        got = N.fast_nl_means_denoising(torch.from_numpy(img).to(device), 15.0, tmpl, search).cpu().numpy()
+    finally:
+        L.call("irx_set_option", b"nlm_v2", 1)
+    for b in range(2):
+        assert np.array_equal(got[b], R.nl_means_u8(img[b], 15.0, tmpl, search)), b
