@@ -20,7 +20,7 @@
 
 namespace irx {
 int g_nlm_strip = 4;                               // irx_set_option("nlm_strip", 4 | 8)
-int g_nlm_v2 = 1;                                  // irx_set_option("nlm_v2", 0): v1 register-window kernel
+int g_nlm_v2 = 1;   // irx_set_option("nlm_v2", v): 1 = v2 centre value from LDS, 2 = v2 centre by DPP, 0 = v1
 namespace {
 
 constexpr int NLM_TW = 32, NLM_G = 8;          // 32 columns x 8 strip groups = 256 threads; strips of S rows
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void nlm_kernel(const uint8_t* __restrict__ sr
 // column slides down one row per dy (one LDS read per offset).
 constexpr int NLM2_WAVES = 4;
 
-template <int CN, int TR, int SR, int S>
+template <int CN, int TR, int SR, int S, bool g_centre_lds>
 __global__ __launch_bounds__(256) void nlm2_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                    int H, int W, int ps, int coff, const int* __restrict__ lut,
                                                    int lut_len, int shift) {
@@ -208,11 +208,16 @@ __global__ __launch_bounds__(256) void nlm2_kernel(const uint8_t* __restrict__ s
         int hs = V[i];
 #pragma unroll
         for (int u = 0; u < 2 * TR; ++u) hs = V[i] + __builtin_amdgcn_update_dpp(0, hs, 0x138, 0xf, 0xf, false);
-        const int q = __builtin_amdgcn_update_dpp(0, nb[i + TR], 0x138, 0xf, 0xf, false);
-        // q is from lane l - 1; the centre needs lane l - TR: shift TR - 1 more times
-        int qc = q;
+        int qc;
+        if (g_centre_lds) {
+          // the centre neighbour sits TR columns left of this lane's own column (lanes < 2TR: discarded;
+          // the index stays inside the region since row a + i + TR >= TR)
+          qc = (int)cb[(a + i + TR) * RW - TR];
+        } else {
+          qc = __builtin_amdgcn_update_dpp(0, nb[i + TR], 0x138, 0xf, 0xf, false);
 #pragma unroll
-        for (int u = 1; u < TR; ++u) qc = __builtin_amdgcn_update_dpp(0, qc, 0x138, 0xf, 0xf, false);
+          for (int u = 1; u < TR; ++u) qc = __builtin_amdgcn_update_dpp(0, qc, 0x138, 0xf, 0xf, false);
+        }
         const int wt = wl[min(hs >> shift, lut_len)];
         wsum[i] += wt;
         if constexpr (CN == 1) {
@@ -248,7 +253,7 @@ void launch2(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int 
   constexpr int PLANE = (TH + 2 * B) * (64 + 2 * SR), PB = CN == 1 ? 1 : 4;
   const size_t lds = ((PLANE * PB + 3) / 4 + lut_len + 1) * sizeof(int);
   IRX_CHECK(lds <= 160 * 1024, "nlmeans: weight table too long for LDS (h too large)");
-  auto k = nlm2_kernel<CN, TR, SR, S>;
+  auto k = g_nlm_v2 == 2 ? nlm2_kernel<CN, TR, SR, S, false> : nlm2_kernel<CN, TR, SR, S, true>;
   if (lds > 64 * 1024) IRX_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                    (int)lds));
   const dim3 grid((W + TWO - 1) / TWO, (H + TH - 1) / TH, N);

@@ -134,3 +134,16 @@ def test_nlm_v1_register_window_bit_exact(device, tmpl, search, cn, shape):
         L.call("irx_set_option", b"nlm_v2", 1)
     for b in range(2):
         assert np.array_equal(got[b], R.nl_means_u8(img[b], 15.0, tmpl, search)), b
+
+
+@pytest.mark.parametrize("tmpl,search", [(3, 5), (7, 21)])
+@pytest.mark.parametrize("cn", [1, 2])
+def test_nlm_v2_dpp_centre_variant_bit_exact(device, tmpl, search, cn):
+    img = _img((2, 37, 130, cn), seed=tmpl * cn)
+    L.call("irx_set_option", b"nlm_v2", 2)
+    try:
+        got = N.fast_nl_means_denoising(torch.from_numpy(img).to(device), 15.0, tmpl, search).cpu().numpy()
+    finally:
+        L.call("irx_set_option", b"nlm_v2", 1)
+    for b in range(2):
+        assert np.array_equal(got[b], R.nl_means_u8(img[b], 15.0, tmpl, search)), b
