@@ -86,18 +86,28 @@ __global__ __launch_bounds__(256) void median_kernel(const uint8_t* __restrict__
     for (int i = 0; i < 5; ++i)
 #pragma unroll
       for (int j = 0; j < 5; ++j) v[i * 5 + j] = tile[c][(ty + i) * RW + tx + j];
-    // the 13th smallest: the value with < 13 smaller and >= 13 smaller-or-equal elements
-    int med = 0;
+    // forgetful selection (buffer of 14 = 25/2 + 2): move the buffer's min to its front and max to its back,
+    // drop both, take the next element; after the last element the one survivor is the 13th smallest
+    int lo = 0, hi = 13;
 #pragma unroll
-    for (int i = 0; i < 25; ++i) {
-      int lt = 0, le = 0;
+    for (int nx = 14; nx <= 25; ++nx) {
 #pragma unroll
-      for (int j = 0; j < 25; ++j) {
-        lt += v[j] < v[i];
-        le += v[j] <= v[i];
+      for (int i = lo + 1; i <= hi; ++i) {
+        const int m = min(v[lo], v[i]);
+        v[i] = max(v[lo], v[i]);
+        v[lo] = m;
       }
-      med = (lt <= 12 && le >= 13) ? v[i] : med;
+#pragma unroll
+      for (int i = lo + 1; i < hi; ++i) {
+        const int M = max(v[i], v[hi]);
+        v[i] = min(v[i], v[hi]);
+        v[hi] = M;
+      }
+      ++lo;
+      --hi;
+      if (nx < 25) v[++hi] = v[nx];
     }
+    const int med = v[lo];
     dst[(((size_t)blockIdx.z * H + y) * W + x) * C + c] = (uint8_t)med;
   }
 }
