@@ -96,6 +96,7 @@ _SIGS = {
     "irx_bilateral_tables": (i32, [i32, C.c_double, C.c_double, i32, vp, vp, vp, i32, C.POINTER(i32),
                                    C.POINTER(i32)]),
     "irx_bilateral_u8": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, i32, vp]),
+    "irx_lab_convert_u8": (i32, [vp, vp, vp, i64, i32]),
     "irx_median_blur_u8": (i32, [vp, vp, vp, i32, i32, i32, i32, i32]),
     "irx_op_conv2d": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32,
                             i32, i32, i32, vp, i64, vp, vp, i32, i32]),

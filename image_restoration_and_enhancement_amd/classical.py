@@ -29,6 +29,10 @@ _M_RGB2XYZ = np.array([[0.412453, 0.357580, 0.180423],
                        [0.212671, 0.715160, 0.072169],
                        [0.019334, 0.119193, 0.950227]])
 _WHITE = np.array([0.950456, 1.0, 1.088754])
+# np.linalg.inv(_M_RGB2XYZ), written out so the host and GPU forms share the exact doubles
+_M_XYZ2RGB = [[3.240481343200526, -1.5371515162713185, -0.4985363261688878],
+              [-0.9692549499965682, 1.8759900014898907, 0.04155592655829284],
+              [0.05564663913517716, -0.20404133836651123, 1.0573110696453443]]
 
 
 def rgb_to_gray_u8(rgb: np.ndarray) -> np.ndarray:
@@ -38,17 +42,21 @@ def rgb_to_gray_u8(rgb: np.ndarray) -> np.ndarray:
 
 
 def rgb_to_lab_u8(rgb: np.ndarray, srgb: bool = True) -> np.ndarray:
-    """8-bit CIELAB as OpenCV stores it: L*255/100, a+128, b+128 (float arithmetic, rounded).
-    srgb=False: the L-variants (COLOR_LRGB2Lab), no gamma linearisation."""
+    """8-bit CIELAB as OpenCV stores it: L*255/100, a+128, b+128 (float64, rounded).
+    srgb=False: the L-variants (COLOR_LRGB2Lab), no gamma linearisation.  Written as explicit elementwise
+    operations in a fixed order (no matmul, whose BLAS summation order is unspecified) so that the GPU form
+    (csrc/filters.hip lab_kernel, fp64 without contraction) computes the same bytes."""
     x = rgb.astype(np.float64) / 255.0
     if srgb:
         x = np.where(x > 0.04045, ((x + 0.055) / 1.055) ** 2.4, x / 12.92)
-    xyz = x @ _M_RGB2XYZ.T / _WHITE
-    f = np.where(xyz > 0.008856, np.cbrt(xyz), 7.787 * xyz + 16.0 / 116.0)
-    L = np.where(xyz[..., 1] > 0.008856, 116.0 * f[..., 1] - 16.0, 903.3 * xyz[..., 1])
-    a = 500.0 * (f[..., 0] - f[..., 1])
-    b = 200.0 * (f[..., 1] - f[..., 2])
-    out = np.stack([L * 255.0 / 100.0, a + 128.0, b + 128.0], -1)
+    r, g, b = x[..., 0], x[..., 1], x[..., 2]
+    M = _M_RGB2XYZ
+    xyz = [(M[i, 0] * r + M[i, 1] * g + M[i, 2] * b) / _WHITE[i] for i in range(3)]
+    f = [np.where(t > 0.008856, np.cbrt(t), 7.787 * t + 16.0 / 116.0) for t in xyz]
+    L = np.where(xyz[1] > 0.008856, 116.0 * f[1] - 16.0, 903.3 * xyz[1])
+    a = 500.0 * (f[0] - f[1])
+    bb = 200.0 * (f[1] - f[2])
+    out = np.stack([L * 255.0 / 100.0, a + 128.0, bb + 128.0], -1)
     return np.clip(np.rint(out), 0, 255).astype(np.uint8)
 
 
@@ -63,6 +71,7 @@ def lab_u8_to_lbgr(lab: np.ndarray) -> np.ndarray:
 
 
 def lab_u8_to_rgb(lab: np.ndarray, srgb: bool = True) -> np.ndarray:
+    """Inverse of rgb_to_lab_u8 (explicit elementwise float64 operations, mirrored by lab_kernel)."""
     L = lab[..., 0].astype(np.float64) * 100.0 / 255.0
     a = lab[..., 1].astype(np.float64) - 128.0
     b = lab[..., 2].astype(np.float64) - 128.0
@@ -70,11 +79,12 @@ def lab_u8_to_rgb(lab: np.ndarray, srgb: bool = True) -> np.ndarray:
     fx, fz = fy + a / 500.0, fy - b / 200.0
 
     def finv(t):
-        return np.where(t > 6.0 / 29.0, t ** 3, (t - 16.0 / 116.0) / 7.787)
+        return np.where(t > 6.0 / 29.0, t * t * t, (t - 16.0 / 116.0) / 7.787)
 
-    y = np.where(L > 903.3 * 0.008856, fy ** 3, L / 903.3)
-    xyz = np.stack([finv(fx), y, finv(fz)], -1) * _WHITE
-    rgb = xyz @ np.linalg.inv(_M_RGB2XYZ).T
+    y = np.where(L > 903.3 * 0.008856, fy * fy * fy, L / 903.3)
+    X, Y, Z = finv(fx) * _WHITE[0], y * _WHITE[1], finv(fz) * _WHITE[2]
+    Mi = _M_XYZ2RGB
+    rgb = np.stack([Mi[i][0] * X + Mi[i][1] * Y + Mi[i][2] * Z for i in range(3)], -1)
     rgb = np.clip(rgb, 0.0, 1.0)
     if srgb:
         rgb = np.where(rgb > 0.0031308, 1.055 * rgb ** (1 / 2.4) - 0.055, 12.92 * rgb)

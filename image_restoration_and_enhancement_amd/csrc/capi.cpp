@@ -388,6 +388,12 @@ int irx_bilateral_u8(void* s, const uint8_t* src, uint8_t* dst, int batch, int H
   if (batch) bilateral_u8(src, dst, batch, H, W, radius, space_w, space_dydx, maxk, color_w, S(s));
   IRX_API_END
 }
+int irx_lab_convert_u8(void* s, const uint8_t* src, uint8_t* dst, long npix, int direction) {
+  IRX_API_BEGIN
+  IRX_CHECK(src && dst && npix >= 0 && (direction == 0 || direction == 1), "bad arguments");
+  if (npix) lab_convert_u8(src, dst, npix, direction, S(s));
+  IRX_API_END
+}
 int irx_median_blur_u8(void* s, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int C, int ksize) {
   IRX_API_BEGIN
   IRX_CHECK(src && dst && src != dst && batch >= 0 && H > 0 && W > 0, "bad arguments");

@@ -112,6 +112,45 @@ __global__ __launch_bounds__(256) void median_kernel(const uint8_t* __restrict__
   }
 }
 
+// 8-bit Lab <-> linear BGR (cv2.COLOR_LBGR2Lab / COLOR_Lab2LBGR as fastNlMeansDenoisingColored applies them),
+// the fp64 restatement of classical.rgb_to_lab_u8(srgb=False) / lab_u8_to_rgb(srgb=False) operation for
+// operation (this file is built without contraction), one thread per pixel.
+__device__ __forceinline__ double lab_f(double t) { return t > 0.008856 ? cbrt(t) : 7.787 * t + 0.13793103448275862; }
+__device__ __forceinline__ double lab_finv(double t) {
+  return t > 0.20689655172413793 ? t * t * t : (t - 0.13793103448275862) / 7.787;
+}
+__device__ __forceinline__ uint8_t sat_rint(double v) { return (uint8_t)fmin(fmax(rint(v), 0.0), 255.0); }
+
+__global__ __launch_bounds__(256) void lab_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                  long npix, int dir) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= npix) return;
+  const uint8_t* s = src + p * 3;
+  uint8_t* o = dst + p * 3;
+  if (dir == 0) {                                             // LBGR -> Lab
+    const double r = s[2] / 255.0, g = s[1] / 255.0, b = s[0] / 255.0;
+    const double X = (0.412453 * r + 0.357580 * g + 0.180423 * b) / 0.950456;
+    const double Y = (0.212671 * r + 0.715160 * g + 0.072169 * b) / 1.0;
+    const double Z = (0.019334 * r + 0.119193 * g + 0.950227 * b) / 1.088754;
+    const double fx = lab_f(X), fy = lab_f(Y), fz = lab_f(Z);
+    const double L = Y > 0.008856 ? 116.0 * fy - 16.0 : 903.3 * Y;
+    o[0] = sat_rint(L * 255.0 / 100.0);
+    o[1] = sat_rint(500.0 * (fx - fy) + 128.0);
+    o[2] = sat_rint(200.0 * (fy - fz) + 128.0);
+  } else {                                                    // Lab -> LBGR
+    const double L = s[0] * 100.0 / 255.0, a = s[1] - 128.0, b = s[2] - 128.0;
+    const double fy = (L + 16.0) / 116.0, fx = fy + a / 500.0, fz = fy - b / 200.0;
+    const double y = L > 7.9996247999999985 ? fy * fy * fy : L / 903.3;
+    const double X = lab_finv(fx) * 0.950456, Y = y * 1.0, Z = lab_finv(fz) * 1.088754;
+    const double R = 3.240481343200526 * X + -1.5371515162713185 * Y + -0.4985363261688878 * Z;
+    const double G = -0.9692549499965682 * X + 1.8759900014898907 * Y + 0.04155592655829284 * Z;
+    const double B = 0.05564663913517716 * X + -0.20404133836651123 * Y + 1.0573110696453443 * Z;
+    o[0] = sat_rint(fmin(fmax(B, 0.0), 1.0) * 255.0);
+    o[1] = sat_rint(fmin(fmax(G, 0.0), 1.0) * 255.0);
+    o[2] = sat_rint(fmin(fmax(R, 0.0), 1.0) * 255.0);
+  }
+}
+
 }  // namespace
 
 void bilateral_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int radius, const float* space_w,
@@ -131,4 +170,12 @@ void median5_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int C, hi
   IRX_HIP(hipGetLastError());
 }
 
+}  // namespace irx
+
+namespace irx {
+void lab_convert_u8(const uint8_t* src, uint8_t* dst, long npix, int dir, hipStream_t s) {
+  ProfScope pr(prof_on() ? std::string("irx::(anonymous namespace)::lab_kernel") : std::string(), 0.0, s);
+  hipLaunchKernelGGL(lab_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, src, dst, npix, dir);
+  IRX_HIP(hipGetLastError());
+}
 }  // namespace irx

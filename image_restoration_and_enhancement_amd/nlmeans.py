@@ -5,8 +5,9 @@ fastNlMeansDenoisingColored (templateWindowSize 7, searchWindowSize 21; csrc/nlm
 
 The invoker (integer patch distances, the weight table, the rounded integer average) is OpenCV's and exact
 against `oracle/nlm_ref.py`.  The colour conversion of the Colored variant (COLOR_LBGR2Lab and back, 8-bit
-Lab; the reference passes RGB bytes where cv2 expects BGR) runs on the host with `classical`'s restatement;
-cv2 is absent from this image, so parity against cv2 itself is unpinned.
+Lab; the reference passes RGB bytes where cv2 expects BGR) is `classical`'s fp64 restatement, run on the GPU
+(`irx_lab_convert_u8`) with the same bytes.  cv2 is absent from this image, so parity against cv2 itself is
+unpinned.
 """
 from __future__ import annotations
 
@@ -82,18 +83,32 @@ def fast_nl_means_denoising_lab(lab: torch.Tensor, h: float, h_color: float, tem
     return out
 
 
-def fast_nl_means_denoising_colored(img: np.ndarray, h: float = 3.0, h_color: float = 3.0,
-                                    template_window_size: int = 7, search_window_size: int = 21,
-                                    device: str = "cuda") -> np.ndarray:
-    """cv2.fastNlMeansDenoisingColored(img, None, h, hColor, 7, 21) for a uint8 [H, W, 3] (or [B, H, W, 3])
-    array: Lab conversion on the host, both invoker passes on the GPU."""
-    from . import classical
-    a = np.asarray(img, dtype=np.uint8)
-    lab = classical.lbgr_to_lab_u8(a)
-    dev = torch.from_numpy(np.ascontiguousarray(lab if lab.ndim == 4 else lab[None])).to(device)
-    out = fast_nl_means_denoising_lab(dev, h, h_color, template_window_size, search_window_size).cpu().numpy()
-    rgb = classical.lab_u8_to_lbgr(out)
-    return rgb if a.ndim == 4 else rgb[0]
+def lab_convert(src: torch.Tensor, direction: int) -> torch.Tensor:
+    """COLOR_LBGR2Lab (direction 0) / COLOR_Lab2LBGR (1) on uint8 [..., 3] CUDA tensors (fp64, exact vs classical)."""
+    x = _check(src)
+    if x.shape[-1] != 3:
+        raise ValueError("expected 3-channel pixels")
+    out = torch.empty_like(x)
+    L.call("irx_lab_convert_u8", C.c_void_p(torch.cuda.current_stream().cuda_stream), C.c_void_p(x.data_ptr()),
+           C.c_void_p(out.data_ptr()), x.numel() // 3, direction)
+    return out
+
+
+def fast_nl_means_denoising_colored(img, h: float = 3.0, h_color: float = 3.0, template_window_size: int = 7,
+                                    search_window_size: int = 21, device: str = "cuda"):
+    """cv2.fastNlMeansDenoisingColored(img, None, h, hColor, 7, 21) for uint8 [H, W, 3] or [B, H, W, 3] images:
+    LBGR -> Lab, L with h, (a, b) with hColor, Lab -> LBGR, all on the GPU.  A CUDA tensor stays on the device;
+    a numpy array is uploaded once and returned as numpy."""
+    is_np = not isinstance(img, torch.Tensor)
+    x = torch.from_numpy(np.ascontiguousarray(img, dtype=np.uint8)).to(device) if is_np else _check(img)
+    single = x.dim() == 3
+    if single:
+        x = x.unsqueeze(0)
+    lab = lab_convert(x, 0)
+    den = fast_nl_means_denoising_lab(lab, h, h_color, template_window_size, search_window_size)
+    out = lab_convert(den, 1)
+    out = out[0] if single else out
+    return out.cpu().numpy() if is_np else out
 
 
 _BIL_CACHE: Dict[Tuple[int, float, float, str], tuple] = {}
@@ -149,14 +164,17 @@ def median_blur(src: torch.Tensor, ksize: int = 5) -> torch.Tensor:
 
 
 def denoise_opencv(image, strength: float, device: str = "cuda"):
-    """RestorationPipeline._denoise_opencv (src/inference.py:500-522) with every filter on the GPU."""
-    from . import classical
-
-    def bil(a, d, sc, ss):
-        return bilateral_filter(torch.from_numpy(np.ascontiguousarray(a)).to(device), d, sc, ss).cpu().numpy()
-
-    def med(a):
-        return median_blur(torch.from_numpy(np.ascontiguousarray(a)).to(device), 5).cpu().numpy()
-
-    return classical.denoise_opencv(image, strength, nlm=lambda *a: fast_nl_means_denoising_colored(*a, device=device),
-                                    bilateral_fn=bil, median_fn=med)
+    """RestorationPipeline._denoise_opencv (src/inference.py:500-522) with every step on the GPU: one upload,
+    Lab conversion, NLM on L and ab, back to BGR, bilateral if strength > 0.6, median if > 0.8, one download."""
+    from PIL import Image
+    img = np.array(image.convert("RGB"))
+    hs = float(np.clip(strength, 0.1, 1.0))
+    h_value = hs * 10 if hs < 0.6 else 20          # luminance strength (src/inference.py:505-507)
+    h_color = hs * 10 if hs < 0.6 else 20
+    x = torch.from_numpy(img).to(device)
+    den = fast_nl_means_denoising_colored(x, h_value, h_color, 7, 21)
+    if strength > 0.6:
+        den = bilateral_filter(den, 9, 75, 75)
+    if strength > 0.8:
+        den = median_blur(den, 5)
+    return Image.fromarray(den.cpu().numpy())

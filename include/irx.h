@@ -178,6 +178,9 @@ int irx_bilateral_tables(int d, double sigma_color, double sigma_space, int cn, 
 /* cv2.bilateralFilter(img, d = 9, ...) on uint8 [batch][H][W][3] (src != dst), tables in device memory. */
 int irx_bilateral_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int radius,
                      const float* space_w, const int* space_dydx, int maxk, const float* color_w);
+/* The colour conversions of cv2.fastNlMeansDenoisingColored (denoising.cpp): direction 0 = COLOR_LBGR2Lab,
+ * 1 = COLOR_Lab2LBGR, 8-bit, `npix` packed 3-byte pixels (in place allowed); fp64, see classical.rgb_to_lab_u8. */
+int irx_lab_convert_u8(void* stream, const uint8_t* src, uint8_t* dst, long npix, int direction);
 /* cv2.medianBlur(img, 5) on uint8 [batch][H][W][C], C <= 4 (src != dst). */
 int irx_median_blur_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int C, int ksize);
 

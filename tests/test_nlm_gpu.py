@@ -147,3 +147,23 @@ def test_nlm_v2_dpp_centre_variant_bit_exact(device, tmpl, search, cn):
         L.call("irx_set_option", b"nlm_v2", 1)
     for b in range(2):
         assert np.array_equal(got[b], R.nl_means_u8(img[b], 15.0, tmpl, search)), b
+
+
+def test_lab_conversion_exhaustive(device):
+    """Every one of the 2^24 byte triplets, both directions, against classical's fp64 restatement."""
+    v = np.arange(1 << 24, dtype=np.uint32)
+    px = np.stack([v & 255, (v >> 8) & 255, v >> 16], -1).astype(np.uint8).reshape(4096, 4096, 3)
+    t = torch.from_numpy(px).to(device)
+    fwd = N.lab_convert(t, 0).cpu().numpy()
+    bad = np.argwhere((fwd != CL.lbgr_to_lab_u8(px)).any(-1))
+    assert len(bad) == 0, (len(bad), px[tuple(bad[0])])
+    inv = N.lab_convert(t, 1).cpu().numpy()
+    bad = np.argwhere((inv != CL.lab_u8_to_lbgr(px)).any(-1))
+    assert len(bad) == 0, (len(bad), px[tuple(bad[0])])
+
+
+def test_colored_device_tensor_path(device):
+    img = _img((2, 40, 52, 3), seed=13)
+    got = N.fast_nl_means_denoising_colored(torch.from_numpy(img).to(device), 10.0, 12.0).cpu().numpy()
+    for b in range(2):
+        assert np.array_equal(got[b], CL.fast_nl_means_denoising_colored(img[b], 10.0, 12.0))
