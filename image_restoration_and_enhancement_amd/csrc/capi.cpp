@@ -394,6 +394,13 @@ int irx_lab_convert_u8(void* s, const uint8_t* src, uint8_t* dst, long npix, int
   if (npix) lab_convert_u8(src, dst, npix, direction, S(s));
   IRX_API_END
 }
+int irx_auto_mask_u8(void* s, const uint8_t* img, int batch, int H, int W, uint8_t* mask, uint8_t* tmp,
+                     int* counts) {
+  IRX_API_BEGIN
+  IRX_CHECK(img && mask && tmp && counts && mask != tmp && batch >= 0 && H > 0 && W > 0, "bad arguments");
+  if (batch) auto_mask_u8(img, batch, H, W, mask, tmp, counts, S(s));
+  IRX_API_END
+}
 int irx_median_blur_u8(void* s, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int C, int ksize) {
   IRX_API_BEGIN
   IRX_CHECK(src && dst && src != dst && batch >= 0 && H > 0 && W > 0, "bad arguments");

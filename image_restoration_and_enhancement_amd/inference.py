@@ -385,7 +385,13 @@ class RestorationPipeline:
         return ip.normalize_mask(mask, target_size)
 
     def _auto_mask_from_image(self, image: Image.Image) -> Image.Image | None:
-        m = classical.auto_mask(image)
+        if self.device.startswith("cuda"):         # threshold + close + open + count on the GPU
+            from . import nlmeans
+            x = torch.from_numpy(np.array(image.convert("RGB"))).to(self.device)
+            mk, keep = nlmeans.auto_mask(x)
+            m = Image.fromarray(mk.cpu().numpy()).convert("L") if keep else None
+        else:
+            m = classical.auto_mask(image)
         if m is None:
             logger.info("No significant damage detected, skipping inpainting")
         return m

@@ -178,3 +178,20 @@ def denoise_opencv(image, strength: float, device: str = "cuda"):
     if strength > 0.8:
         den = median_blur(den, 5)
     return Image.fromarray(den.cpu().numpy())
+
+
+def auto_mask(img: torch.Tensor):
+    """_auto_mask_from_image (src/inference.py:805-840) on uint8 RGB CUDA images [H, W, 3] or [B, H, W, 3]:
+    returns (masks uint8 [.., H, W] with 255 = damaged, keep bool per image = non-zero share >= 1 %)."""
+    x = _check(img)
+    single = x.dim() == 3
+    if single:
+        x = x.unsqueeze(0)
+    B, H, W, _ = x.shape
+    mask = torch.empty((B, H, W), dtype=torch.uint8, device=x.device)
+    tmp = torch.empty_like(mask)
+    counts = torch.empty(B, dtype=torch.int32, device=x.device)
+    L.call("irx_auto_mask_u8", C.c_void_p(torch.cuda.current_stream().cuda_stream), C.c_void_p(x.data_ptr()), B, H,
+           W, C.c_void_p(mask.data_ptr()), C.c_void_p(tmp.data_ptr()), C.c_void_p(counts.data_ptr()))
+    keep = [int(c) / (H * W) >= 0.01 for c in counts.cpu().tolist()]
+    return (mask[0], keep[0]) if single else (mask, keep)

@@ -181,6 +181,11 @@ int irx_bilateral_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch, 
 /* The colour conversions of cv2.fastNlMeansDenoisingColored (denoising.cpp): direction 0 = COLOR_LBGR2Lab,
  * 1 = COLOR_Lab2LBGR, 8-bit, `npix` packed 3-byte pixels (in place allowed); fp64, see classical.rgb_to_lab_u8. */
 int irx_lab_convert_u8(void* stream, const uint8_t* src, uint8_t* dst, long npix, int direction);
+/* _auto_mask_from_image (src/inference.py:805-840) for uint8 RGB [batch][H][W][3]: mask [batch][H][W] (255 = damaged)
+ * after MORPH_CLOSE + MORPH_OPEN (5x5), counts[batch] = its non-zero pixels (device int); tmp = [batch][H][W]
+ * scratch.  The caller applies the reference's 1 % rule. */
+int irx_auto_mask_u8(void* stream, const uint8_t* img, int batch, int H, int W, uint8_t* mask, uint8_t* tmp,
+                     int* counts);
 /* cv2.medianBlur(img, 5) on uint8 [batch][H][W][C], C <= 4 (src != dst). */
 int irx_median_blur_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int C, int ksize);
 

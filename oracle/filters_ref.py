@@ -58,3 +58,24 @@ def median5_u8(img: np.ndarray) -> np.ndarray:
     pad = np.pad(img, ((2, 2), (2, 2), (0, 0)), mode="edge")
     win = np.stack([pad[i:i + H, j:j + W] for i in range(5) for j in range(5)], 0)
     return np.sort(win, axis=0)[12].astype(np.uint8)
+
+
+def _morph5(m: np.ndarray, op: str) -> np.ndarray:
+    """5x5 square dilation ('max', border 0) or erosion ('min', border 255) — OpenCV's default border value."""
+    H, W = m.shape
+    fill = 0 if op == "max" else 255
+    pad = np.full((H + 4, W + 4), fill, np.uint8)
+    pad[2:-2, 2:-2] = m
+    win = np.stack([pad[i:i + H, j:j + W] for i in range(5) for j in range(5)], 0)
+    return win.max(0) if op == "max" else win.min(0)
+
+
+def auto_mask_u8(rgb: np.ndarray):
+    """_auto_mask_from_image (src/inference.py:805-840): RGB2GRAY fixed point, THRESH_BINARY_INV at 30 |
+    THRESH_BINARY at 225, MORPH_CLOSE then MORPH_OPEN (5x5 ones); returns (mask, keep = share >= 1 %)."""
+    r, g, b = (rgb[..., i].astype(np.int64) for i in range(3))
+    gray = (r * 4899 + g * 9617 + b * 1868 + (1 << 13)) >> 14
+    m = np.where((gray <= 30) | (gray > 225), 255, 0).astype(np.uint8)
+    m = _morph5(_morph5(m, "max"), "min")
+    m = _morph5(_morph5(m, "min"), "max")
+    return m, np.sum(m > 0) / m.size >= 0.01

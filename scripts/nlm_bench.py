@@ -68,6 +68,23 @@ for name, fn in (("bilateral_9_75_75", lambda: N.bilateral_filter(rgb, 9, 75, 75
     e1.record()
     torch.cuda.synchronize()
     res[name + "_ms_per_batch"] = round(e0.elapsed_time(e1) / a.iters, 3)
+# the whole classical denoise chain at strength 0.9 on the batch (device-resident): LBGR->Lab, NLM L + ab,
+# Lab->LBGR, bilateral(9, 75, 75), median(5) -- what RestorationPipeline._denoise_opencv runs per image
+def chain():
+    d = N.fast_nl_means_denoising_colored(rgb, 20.0, 20.0)
+    return N.median_blur(N.bilateral_filter(d, 9, 75, 75), 5)
+
+
+chain()
+torch.cuda.synchronize()
+e0.record()
+for _ in range(a.iters):
+    chain()
+e1.record()
+torch.cuda.synchronize()
+cms = e0.elapsed_time(e1) / a.iters
+res["denoise_chain_ms_per_batch"] = round(cms, 3)
+res["denoise_chain_images_per_s"] = round(a.batch / (cms / 1e3), 1)
 if a.cpu:
     t = time.time()
     img = noisy[0]
@@ -75,4 +92,8 @@ if a.cpu:
     CL.nl_means_u8(img[..., 1:], 20.0)
     res["cpu_baseline"] = {"value": round(1 / (time.time() - t), 4), "unit": "images/s", "cores": 1,
                            "kind": "port", "sample": f"1 image {a.size}^2, classical.nl_means_u8 (numpy)"}
+    from PIL import Image
+    t = time.time()
+    CL.denoise_opencv(Image.fromarray(noisy[0]), 0.9)
+    res["cpu_denoise_chain_images_per_s"] = round(1 / (time.time() - t), 4)
 print(json.dumps(res))

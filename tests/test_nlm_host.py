@@ -70,3 +70,15 @@ def test_classical_filters_match_oracle():
     a = np.random.default_rng(8).integers(0, 256, (23, 30, 3), dtype=np.uint8)
     assert np.array_equal(CL.bilateral(a), F.bilateral_u8(a))
     assert np.array_equal(CL.median5(a), F.median5_u8(a))
+
+
+def test_classical_auto_mask_matches_oracle():
+    from oracle import filters_ref as F
+    rng = np.random.default_rng(21)
+    img = rng.integers(40, 200, (50, 61, 3), dtype=np.uint8)
+    img[5:12, 7:30] = 5
+    img[30:34, 40:58] = 250
+    img[44, 3] = 0                                        # a speck the opening removes
+    m, keep = F.auto_mask_u8(img)
+    got = CL.auto_mask(__import__("PIL.Image", fromlist=["Image"]).fromarray(img))
+    assert keep and got is not None and np.array_equal(np.array(got), m) and m[44, 3] == 0
