@@ -98,6 +98,7 @@ _SIGS = {
     "irx_bilateral_u8": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, i32, vp]),
     "irx_lab_convert_u8": (i32, [vp, vp, vp, i64, i32]),
     "irx_auto_mask_u8": (i32, [vp, vp, i32, i32, i32, vp, vp, vp]),
+    "irx_colorize_lab_u8": (i32, [vp, vp, i64, vp, vp, vp]),
     "irx_median_blur_u8": (i32, [vp, vp, vp, i32, i32, i32, i32, i32]),
     "irx_op_conv2d": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32,
                             i32, i32, i32, vp, i64, vp, vp, i32, i32]),

@@ -210,13 +210,24 @@ def sr_lanczos(image: Image.Image, scale: int) -> Image.Image:
     return image.resize((w * scale, h * scale), Image.LANCZOS)
 
 
-def colorize_lab(image: Image.Image) -> Image.Image:
-    img = np.array(image.convert("RGB"))
-    L = rgb_to_lab_u8(img)[..., 0]
+def colorize_from_L(L: np.ndarray) -> np.ndarray:
+    """src/inference.py:683-703 after the L channel: a = L*0.1-10, b = L*0.1-5 as int8 (negative values wrap
+    through the uint8 cast exactly as the reference's `astype(np.uint8)` does), LAB -> RGB."""
     a = np.clip(L * 0.1 - 10, -127, 127).astype(np.int8)
     b = np.clip(L * 0.1 - 5, -127, 127).astype(np.int8)
-    lab = np.stack([L, a, b], axis=2)             # int8 promotes; the uint8 cast below wraps negatives
-    return Image.fromarray(lab_u8_to_rgb(lab.astype(np.uint8)))
+    lab = np.stack([L, a, b], axis=-1)            # int8 promotes; the uint8 cast below wraps negatives
+    return lab_u8_to_rgb(lab.astype(np.uint8))
+
+
+def srgb_linear_lut() -> np.ndarray:
+    """The sRGB linearisation of rgb_to_lab_u8 for the 256 byte values (same elementwise numpy operations)."""
+    x = np.arange(256).astype(np.float64) / 255.0
+    return np.where(x > 0.04045, ((x + 0.055) / 1.055) ** 2.4, x / 12.92)
+
+
+def colorize_lab(image: Image.Image) -> Image.Image:
+    img = np.array(image.convert("RGB"))
+    return Image.fromarray(colorize_from_L(rgb_to_lab_u8(img)[..., 0]))
 
 
 def auto_mask(image: Image.Image) -> Optional[Image.Image]:

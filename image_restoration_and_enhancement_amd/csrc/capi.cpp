@@ -401,6 +401,13 @@ int irx_auto_mask_u8(void* s, const uint8_t* img, int batch, int H, int W, uint8
   if (batch) auto_mask_u8(img, batch, H, W, mask, tmp, counts, S(s));
   IRX_API_END
 }
+int irx_colorize_lab_u8(void* s, const uint8_t* img, long npix, const double* lin_lut, const uint8_t* color_map,
+                        uint8_t* out) {
+  IRX_API_BEGIN
+  IRX_CHECK(img && lin_lut && color_map && out && npix >= 0, "bad arguments");
+  if (npix) colorize_lab_u8(img, npix, lin_lut, color_map, out, S(s));
+  IRX_API_END
+}
 int irx_median_blur_u8(void* s, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int C, int ksize) {
   IRX_API_BEGIN
   IRX_CHECK(src && dst && src != dst && batch >= 0 && H > 0 && W > 0, "bad arguments");

@@ -243,3 +243,34 @@ void auto_mask_u8(const uint8_t* img, int B, int H, int W, uint8_t* mask, uint8_
   }
 }
 }  // namespace irx
+
+// ------------------------------------------------------------------------------------------------------
+// _colorize_lab (src/inference.py:683-703): L of RGB2LAB (sRGB), then a fixed L -> RGB colour map.  The
+// colour map has only 256 entries and the sRGB linearisation only 256 inputs, so both come from the host's
+// fp64 restatement (classical.colorize_from_L / srgb_linear_lut) as tables; the kernel computes L in fp64
+// operation for operation (Y row of the RGB->XYZ matrix, cube root, CIE L*, * 255 / 100, rint).
+namespace irx {
+namespace {
+__global__ __launch_bounds__(256) void colorize_kernel(const uint8_t* __restrict__ img, long npix,
+                                                       const double* __restrict__ lin, const uint8_t* __restrict__ cmap,
+                                                       uint8_t* __restrict__ out) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= npix) return;
+  const uint8_t* q = img + p * 3;
+  const double r = lin[q[0]], g = lin[q[1]], b = lin[q[2]];
+  const double Y = (0.212671 * r + 0.715160 * g + 0.072169 * b) / 1.0;
+  const double L = Y > 0.008856 ? 116.0 * lab_f(Y) - 16.0 : 903.3 * Y;
+  const int l = sat_rint(L * 255.0 / 100.0);
+  out[p * 3 + 0] = cmap[l * 3 + 0];
+  out[p * 3 + 1] = cmap[l * 3 + 1];
+  out[p * 3 + 2] = cmap[l * 3 + 2];
+}
+}  // namespace
+
+void colorize_lab_u8(const uint8_t* img, long npix, const double* lin, const uint8_t* cmap, uint8_t* out,
+                     hipStream_t s) {
+  ProfScope pr(prof_on() ? std::string("irx::(anonymous namespace)::colorize_kernel") : std::string(), 0.0, s);
+  hipLaunchKernelGGL(colorize_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, img, npix, lin, cmap, out);
+  IRX_HIP(hipGetLastError());
+}
+}  // namespace irx

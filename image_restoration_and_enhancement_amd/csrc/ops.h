@@ -156,6 +156,8 @@ void bilateral_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int rad
                   const int* space_dydx, int maxk, const float* color_w, hipStream_t s);
 void lab_convert_u8(const uint8_t* src, uint8_t* dst, long npix, int dir, hipStream_t s);
 void auto_mask_u8(const uint8_t* img, int B, int H, int W, uint8_t* mask, uint8_t* tmp, int* counts, hipStream_t s);
+void colorize_lab_u8(const uint8_t* img, long npix, const double* lin, const uint8_t* cmap, uint8_t* out,
+                     hipStream_t s);
 void median5_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int C, hipStream_t s);
 
 }  // namespace irx

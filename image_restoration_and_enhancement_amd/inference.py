@@ -347,7 +347,13 @@ class RestorationPipeline:
 
     def _colorize_lab(self, image: Image.Image) -> Image.Image:
         try:
+            if self.device.startswith("cuda"):     # L + 256-entry colour map on the GPU (same bytes)
+                from . import nlmeans
+                x = torch.from_numpy(np.array(image.convert("RGB"))).to(self.device)
+                return Image.fromarray(nlmeans.colorize_lab(x).cpu().numpy())
             return classical.colorize_lab(image)
+        except IrxError:
+            raise
         except Exception as e:
             logger.warning(f"LAB colorization failed: {e}, returning grayscale as RGB")
             return image

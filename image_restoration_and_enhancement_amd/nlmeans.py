@@ -195,3 +195,24 @@ def auto_mask(img: torch.Tensor):
            W, C.c_void_p(mask.data_ptr()), C.c_void_p(tmp.data_ptr()), C.c_void_p(counts.data_ptr()))
     keep = [int(c) / (H * W) >= 0.01 for c in counts.cpu().tolist()]
     return (mask[0], keep[0]) if single else (mask, keep)
+
+
+_COLOR_TABLES: Dict[str, tuple] = {}
+
+
+def colorize_lab(img: torch.Tensor) -> torch.Tensor:
+    """_colorize_lab (src/inference.py:683-703) on uint8 RGB CUDA images [..., 3]; same bytes as
+    classical.colorize_lab (the 256-entry tables come from its fp64 restatement)."""
+    from . import classical
+    x = _check(img)
+    key = str(x.device)
+    if key not in _COLOR_TABLES:
+        lin = torch.from_numpy(classical.srgb_linear_lut()).to(x.device)
+        cmap = torch.from_numpy(np.ascontiguousarray(classical.colorize_from_L(np.arange(256, dtype=np.uint8)))).to(
+            x.device)
+        _COLOR_TABLES[key] = (lin, cmap)
+    lin, cmap = _COLOR_TABLES[key]
+    out = torch.empty_like(x)
+    L.call("irx_colorize_lab_u8", C.c_void_p(torch.cuda.current_stream().cuda_stream), C.c_void_p(x.data_ptr()),
+           x.numel() // 3, C.c_void_p(lin.data_ptr()), C.c_void_p(cmap.data_ptr()), C.c_void_p(out.data_ptr()))
+    return out

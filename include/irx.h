@@ -186,6 +186,10 @@ int irx_lab_convert_u8(void* stream, const uint8_t* src, uint8_t* dst, long npix
  * scratch.  The caller applies the reference's 1 % rule. */
 int irx_auto_mask_u8(void* stream, const uint8_t* img, int batch, int H, int W, uint8_t* mask, uint8_t* tmp,
                      int* counts);
+/* _colorize_lab (src/inference.py:683-703) for `npix` RGB pixels: L of RGB2LAB (sRGB) via lin_lut[256] (device
+ * doubles, the sRGB linearisation of each byte value), then out = color_map[L] (device uint8 [256][3]). */
+int irx_colorize_lab_u8(void* stream, const uint8_t* img, long npix, const double* lin_lut, const uint8_t* color_map,
+                        uint8_t* out);
 /* cv2.medianBlur(img, 5) on uint8 [batch][H][W][C], C <= 4 (src != dst). */
 int irx_median_blur_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int C, int ksize);
 
