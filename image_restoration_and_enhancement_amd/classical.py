@@ -92,15 +92,6 @@ def lab_u8_to_rgb(lab: np.ndarray, srgb: bool = True) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------------------- filters
-def _box_sum(x: np.ndarray, r: int) -> np.ndarray:
-    """Sum over a (2r+1)^2 window of a reflect-101 padded [H, W] array."""
-    p = np.pad(x, r, mode="reflect")
-    c = np.cumsum(np.cumsum(p, 0), 1)
-    c = np.pad(c, ((1, 0), (1, 0)))
-    k = 2 * r + 1
-    return c[k:, k:] - c[:-k, k:] - c[k:, :-k] + c[:-k, :-k]
-
-
 def nlm_weights(h: float, cn: int, template: int = 7, search: int = 21) -> np.ndarray:
     """OpenCV FastNlMeansDenoisingInvoker's weight table: w[a] = cvRound(fpm * exp(-a * 2^s / template^2 /
     (f32(h)^2 * cn))), zero below 0.001 * fpm, fpm = INT_MAX // (search^2 * 255), 2^s >= template^2."""
