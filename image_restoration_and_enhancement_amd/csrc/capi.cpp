@@ -73,6 +73,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gemm_small_kmax") g_gemm_small_kmax = value;
   else if (n == "nlm_strip") g_nlm_strip = value;
   else if (n == "nlm_v2") g_nlm_v2 = value;
+  else if (n == "nlm2_strip") g_nlm2_strip = value;
   else throw Error("unknown option " + n);
   IRX_API_END
 }

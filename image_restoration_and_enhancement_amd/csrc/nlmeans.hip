@@ -20,6 +20,7 @@
 
 namespace irx {
 int g_nlm_strip = 4;                               // irx_set_option("nlm_strip", 4 | 8)
+int g_nlm2_strip = 4;                              // irx_set_option("nlm2_strip", 2 | 4 | 8 | 16)
 int g_nlm_v2 = 1;   // irx_set_option("nlm_v2", v): 1 = v2 centre value from LDS, 2 = v2 centre by DPP, 0 = v1
 namespace {
 
@@ -246,14 +247,15 @@ __global__ __launch_bounds__(256) void nlm2_kernel(const uint8_t* __restrict__ s
   }
 }
 
-template <int CN, int TR, int SR>
-void launch2(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, const int* lut, int lut_len,
-             int shift, hipStream_t s) {
-  constexpr int S = 8, TWO = 64 - 2 * TR, TH = NLM2_WAVES * S, B = TR + SR;
+template <int CN, int TR, int SR, int S>
+void launch2s(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, const int* lut, int lut_len,
+              int shift, hipStream_t s) {
+  constexpr int TWO = 64 - 2 * TR, TH = NLM2_WAVES * S, B = TR + SR;
   constexpr int PLANE = (TH + 2 * B) * (64 + 2 * SR), PB = CN == 1 ? 1 : 4;
   const size_t lds = ((PLANE * PB + 3) / 4 + lut_len + 1) * sizeof(int);
   IRX_CHECK(lds <= 160 * 1024, "nlmeans: weight table too long for LDS (h too large)");
   auto k = g_nlm_v2 == 2 ? nlm2_kernel<CN, TR, SR, S, false> : nlm2_kernel<CN, TR, SR, S, true>;
+  static_assert(S >= 1, "strip rows");
   if (lds > 64 * 1024) IRX_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                    (int)lds));
   const dim3 grid((W + TWO - 1) / TWO, (H + TH - 1) / TH, N);
@@ -261,6 +263,17 @@ void launch2(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int 
   ProfScope pr(prof_on() ? std::string("irx::(anonymous namespace)::nlm2_kernel") : std::string(), ops, s);
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, src, dst, H, W, ps, coff, lut, lut_len, shift);
   IRX_HIP(hipGetLastError());
+}
+
+template <int CN, int TR, int SR>
+void launch2(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, const int* lut, int lut_len,
+             int shift, hipStream_t s) {
+  // strip rows per wave: 4 (default; measured 1.29 vs 1.40 / 1.67 ms per 8x512^2 batch for 8 / 16) or 2 / 8 / 16
+  // (irx_set_option("nlm2_strip", ...))
+  if (g_nlm2_strip == 2) return launch2s<CN, TR, SR, 2>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+  if (g_nlm2_strip == 8) return launch2s<CN, TR, SR, 8>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+  if (g_nlm2_strip == 16) return launch2s<CN, TR, SR, 16>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
+  return launch2s<CN, TR, SR, 4>(src, dst, N, H, W, ps, coff, lut, lut_len, shift, s);
 }
 
 template <int CN, int TR, int SR, int NLM_S>

@@ -148,7 +148,7 @@ void degrade_strokes(int B, int H, int W, const int* segs, const int* thick, con
 
 
 // ------------------------------------------------------------ fast non-local means (nlmeans.hip)
-extern int g_nlm_strip, g_nlm_v2;
+extern int g_nlm_strip, g_nlm_v2, g_nlm2_strip;
 void nlmeans_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int ps, int coff, int cn, int tmpl,
                 int search, const int* lut, int lut_len, int shift, hipStream_t s);
 // ------------------------------------------------------------ bilateral / median (filters.hip)

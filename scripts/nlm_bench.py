@@ -23,10 +23,13 @@ ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--cpu", action="store_true")
 ap.add_argument("--strip", type=int, default=0, help="irx option nlm_strip (0: library default)")
 ap.add_argument("--v2", type=int, default=-1, help="irx option nlm_v2 (-1: library default)")
+ap.add_argument("--strip2", type=int, default=0, help="irx option nlm2_strip (0: library default)")
 a = ap.parse_args()
 
 if a.v2 >= 0:
     L.call("irx_set_option", b"nlm_v2", a.v2)
+if a.strip2:
+    L.call("irx_set_option", b"nlm2_strip", a.strip2)
 if a.strip:
     L.call("irx_set_option", b"nlm_strip", a.strip)
 rng = np.random.default_rng(0)

@@ -220,3 +220,16 @@ def test_pipeline_colorize_fallback_runs_gpu(device):
     p.device = "cuda"
     img = Image.fromarray(_img((33, 47, 3), seed=17))
     assert np.array_equal(np.array(p._colorize_lab(img)), np.array(CL.colorize_lab(img)))
+
+
+@pytest.mark.parametrize("strip", [2, 8, 16])
+@pytest.mark.parametrize("cn", [1, 2])
+def test_nlm_v2_strip_variants_bit_exact(device, strip, cn):
+    img = _img((2, 70, 130, cn), seed=strip + cn)
+    L.call("irx_set_option", b"nlm2_strip", strip)
+    try:
+        got = N.fast_nl_means_denoising(torch.from_numpy(img).to(device), 15.0).cpu().numpy()
+    finally:
+        L.call("irx_set_option", b"nlm2_strip", 4)
+    for b in range(2):
+        assert np.array_equal(got[b], R.nl_means_u8(img[b], 15.0)), b
