@@ -1,25 +1,40 @@
 #!/usr/bin/env python3
 """Throughput benchmark of the MI355X restoration engine (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): the reference's denoise task — SD-1.5 img2img at 512x512,
-batch 8 images per GPU, 50 DDIM steps at strength 0.5 (25 UNet evaluations, classifier-free
-guidance 5.0 -> UNet batch 16), bf16, seeded random weights of the SD-1.5 architecture (no
-checkpoints are available offline), synthetic noisy images.  One "step" is one full pass of the hot
-path over one batch: uint8 pixels resident in HBM -> CLIP text encoding -> VAE encode -> posterior
-sample + add_noise -> 25 x (UNet + fused CFG/DDIM step) -> VAE decode -> uint8 pixels.
+Default workload (BASELINE.json configs[1]): the reference's denoise task — SD-1.5 img2img at
+512x512, batch 8 images per GPU, 50 DDIM steps at strength 0.5 (25 UNet evaluations, classifier-free
+guidance 5.0 -> UNet batch 16), bf16, seeded random weights of the SD-1.5 architecture (no checkpoints
+are available offline), synthetic noisy images.  One "step" is one full pass of the hot path over one
+batch: uint8 pixels resident in HBM -> CLIP text encoding -> VAE encode -> posterior sample + add_noise
+-> n x (UNet + fused CFG/scheduler step) -> VAE decode -> uint8 pixels.
 
-`python bench.py --gpus N --steps K --warmup W` (N > 1 under torch.distributed.run, one rank per
-GPU, weak scaling: 8 images per rank).  Rank 0 prints one JSON line.  Also reported:
-  roofline     — the dominant MFMA kernel's algorithmic TFLOP/s (HIP events around every launch
-                 of it during a profiled repeat of the timed steps) against the 2.5 PF bf16 dense peak;
-  cpu_baseline — the fp32 PyTorch-CPU restatement of the reference path (oracle/, the reference's
-                 own CPU path through diffusers cannot run here), timed on a bounded sample on the
-                 host cores (rank 0, N = 1 only).
+`--task` selects the other BASELINE configs as per-GPU shards (weak scaling; N > 1 under
+torch.distributed.run, one rank per GPU):
+  sr        configs[2]: sr_x4 128 -> 512 (bicubic pre-upscale), batch 16, strength 0.8, no CFG, 40 evals
+  inpaint   configs[3]: 512x512 + stroke masks, 8 images per GPU (32 over 4 GPUs), 9-channel UNet,
+            strength 0.6, CFG 5.0, 30 evals, two VAE encodes
+  colorize  configs[4]: 768x768 gray, 8 images per GPU (64 over 8 GPUs), fp16, strength 0.75, CFG 7.5,
+            37 evals
+Algorithmic work per image comes from BASELINE.md §2 (per-resolution UNet / VAE GFLOP, attention
+quadratic in the token count), not a (res/512)^2 scaling.
+
+Also reported (rank 0):
+  roofline     — the dominant MFMA kernel's algorithmic TFLOP/s (HIP events around every launch of it
+                 during a profiled repeat of the timed steps) against the dense MFMA peak;
+  cpu_baseline — BASELINE.md §3: the reference CPU path (fp32 PyTorch-CPU restatement, oracle/ — the
+                 reference's own diffusers path cannot run here) on configs[0]: full 512x512 denoise
+                 images, 20 PNDM steps x strength 0.5 (11 UNet evals, CFG), on this process's usable
+                 host cores (N = 1 only);
+  parity       — the same configs[0] image through the GPU engine (fp32 and bf16): max |decoded pixel
+                 difference| of the fp32 engine vs the CPU reference, PSNR/SSIM (metrics.py, pinned to
+                 scikit-image) of the bf16 output vs the CPU reference output and of both vs the clean
+                 ground truth.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -37,29 +52,78 @@ from image_restoration_and_enhancement_amd import weights as W  # noqa: E402
 from image_restoration_and_enhancement_amd.configs import PipelineConfig  # noqa: E402
 from image_restoration_and_enhancement_amd.pipelines import SDEngine, draw_noise  # noqa: E402
 
-PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec; no sparsity)
-PEAK_F32_TFLOPS = 157.3
-PROMPT = "clean high quality photo, no noise, sharp details"       # src/inference.py:87
-# algorithmic GFLOP per unit (SURVEY.md §8d / BASELINE.md §2, 2*MAC over conv + linear + attention)
-F_UNET_512, F_ENC_512, F_DEC_512 = 808.0, 1118.7, 2518.3
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}   # MI355X dense (MI355X_MICROARCH.md)
+# algorithmic GFLOP per unit (2*MAC over conv + linear + attention QK^T / PV)
+F_UNET = {128: 45.9, 512: 808.0, 768: 2168.9}
+F_ENC = {128: 67.9, 512: 1118.7, 768: 2613.9}
+F_DEC = {128: 155.4, 512: 2518.3, 768: 5763.0}
+PROMPTS = {   # src/inference.py:86-91
+    "denoise": "clean high quality photo, no noise, sharp details",
+    "sr": "high quality, detailed, sharp",
+    "colorize": "vibrant realistic natural colors, colorful, high quality photo, detailed, full color, rich colors",
+    "inpaint": "high quality detailed photo",
+}
+# BASELINE.json configs[1..4] as per-GPU workloads
+TASKS = {
+    "denoise": dict(cfg=2, res=512, batch=8, strength=0.5, guidance=5.0, dtype="bf16", n_enc=1),
+    "sr": dict(cfg=3, res=512, lr=128, batch=16, strength=0.8, guidance=0.0, dtype="bf16", n_enc=1),
+    "inpaint": dict(cfg=4, res=512, batch=8, strength=0.6, guidance=5.0, dtype="bf16", n_enc=2),
+    "colorize": dict(cfg=5, res=768, batch=8, strength=0.75, guidance=7.5, dtype="fp16", n_enc=1),
+}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def synthetic_batch(n: int, res: int, seed: int) -> np.ndarray:
-    """Smooth structured images + Gaussian noise sigma in [5, 8] (scripts/make_synthetic_pairs.py:29-35)."""
+def synthetic_pairs(n: int, res: int, seed: int):
+    """(clean, noisy) uint8 [n, res, res, 3]: smooth structured images + Gaussian noise sigma in [5, 8]
+    (scripts/make_synthetic_pairs.py:29-35)."""
     rng = np.random.default_rng(seed)
     yy, xx = np.mgrid[0:res, 0:res].astype(np.float32)
-    out = []
-    for i in range(n):
+    clean, noisy = [], []
+    for _ in range(n):
         f = rng.uniform(0.01, 0.05, size=(3, 2))
         ph = rng.uniform(0, 6.28, size=3)
         img = np.stack([128 + 100 * np.sin(f[c, 0] * xx + f[c, 1] * yy + ph[c]) for c in range(3)], -1)
+        clean.append(np.clip(img, 0, 255).astype(np.uint8))
         img = img + rng.normal(0, rng.uniform(5, 8), img.shape)
-        out.append(np.clip(img, 0, 255).astype(np.uint8))
-    return np.stack(out)
+        noisy.append(np.clip(img, 0, 255).astype(np.uint8))
+    return np.stack(clean), np.stack(noisy)
+
+
+def stroke_masks(n: int, res: int, seed: int) -> np.ndarray:
+    """Free-form stroke masks {0, 1} (scripts/make_synthetic_pairs.py:104-114 shape statistics)."""
+    rng = np.random.default_rng(seed)
+    out = np.zeros((n, res, res), np.float32)
+    for i in range(n):
+        for _ in range(rng.integers(2, 5)):
+            y, x = rng.integers(0, res, size=2)
+            r = int(rng.integers(res // 64, res // 24))
+            for _ in range(int(rng.integers(8, 20))):
+                y = int(np.clip(y + rng.integers(-res // 16, res // 16), 0, res - 1))
+                x = int(np.clip(x + rng.integers(-res // 16, res // 16), 0, res - 1))
+                out[i, max(0, y - r):y + r, max(0, x - r):x + r] = 1.0
+    return out
+
+
+def task_inputs(task: str, spec: dict, batch: int, seed: int):
+    """Per-task synthetic batch in host memory: (uint8 [B, H, W, 3], optional fp32 mask [B, H, W])."""
+    res = spec["res"]
+    if task == "sr":
+        # LR 128x128 (blurred, 4x down) bicubic pre-upscaled to 512 before img2img
+        _, lr = synthetic_pairs(batch, spec["lr"], seed)
+        t = torch.from_numpy(lr).permute(0, 3, 1, 2).float()
+        up = torch.nn.functional.interpolate(t, size=(res, res), mode="bicubic", align_corners=False)
+        return up.round().clamp(0, 255).to(torch.uint8).permute(0, 2, 3, 1).numpy(), None
+    clean, noisy = synthetic_pairs(batch, res, seed)
+    if task == "colorize":
+        gray = (0.299 * clean[..., 0] + 0.587 * clean[..., 1] + 0.114 * clean[..., 2]).round().astype(np.uint8)
+        return np.repeat(gray[..., None], 3, axis=3), None
+    if task == "inpaint":
+        m = stroke_masks(batch, res, seed)
+        return (clean * (1 - m[..., None])).astype(np.uint8), m
+    return noisy, None
 
 
 def build_engine(cfg, dtype, device, rank):
@@ -80,40 +144,101 @@ def build_engine(cfg, dtype, device, rank):
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (scripts/pmc_traffic.py;
     FETCH_SIZE x2 + WRITE_SIZE per the gfx950 note), or None when no pass for this kernel is committed."""
-    for f in sorted(Path(__file__).resolve().parent.glob("profiles/*pmc_traffic*.json"), reverse=True):
+    for f in sorted(ROOT.glob("profiles/*pmc_traffic*.json"), reverse=True):
         try:
             d = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
-        if d.get("kernel") and d["kernel"] in kernel:
+        if d.get("kernel") and kernel.endswith("::" + d["kernel"]):
             return round(d["bytes_per_launch"])
     return None
 
 
-def cpu_baseline(cfg, sds, res: int, steps: int, strength: float, threads: int) -> dict:
-    """fp32 CPU restatement: 1 image; VAE encode + 1 CFG UNet eval (batch 2) + VAE decode, extrapolated
-    to the full per-image schedule (n_evals UNet evals)."""
-    from oracle import sd_ref
+def usable_cpus() -> int:
+    """CPUs this process may run on: sched affinity, capped by a cgroup CPU quota when one is set."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            n = min(n, max(1, math.ceil(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_and_parity(eng_bf16, sds, device, n_images: int, threads: int) -> tuple:
+    """configs[0] on the host cores through the fp32 CPU restatement, plus the same images
+    through the GPU engine (fp32 and bf16) for the parity report."""
+    from image_restoration_and_enhancement_amd import metrics as M
+    from oracle import pipeline_ref as PR
+    from image_restoration_and_enhancement_amd.tokenizer import PromptTokenizer
+    from PIL import Image
+
+    prompt, strength, steps, guidance = PR.TASKS["denoise"]
+    cfg = PipelineConfig.default("denoise")               # saved scheduler: PNDM (configs[0])
+    tok = PromptTokenizer()
+    ids_p, ids_n = torch.from_numpy(tok(prompt))[None], torch.from_numpy(tok(""))[None]
+    models = PR.Models(sds["unet"], cfg.unet, sds["vae"], cfg.vae, sds["clip"], cfg.clip)
+    clean, noisy = synthetic_pairs(n_images, 512, seed=1000)
     torch.set_num_threads(threads)
-    n_evals = min(int(steps * strength), steps)
-    h = res // 8
-    g = torch.Generator().manual_seed(0)
-    img = torch.rand(1, 3, res, res, generator=g) * 2 - 1
-    ctx = torch.randn(2, 77, 768, generator=g)
+    refs, t_img = [], []
     with torch.no_grad():
-        t0 = time.perf_counter()
-        mom = sd_ref.vae_encode_moments(sds["vae"], cfg.vae, img)
-        t1 = time.perf_counter()
-        x = torch.randn(2, 4, h, h, generator=g)
-        sd_ref.unet_forward(sds["unet"], cfg.unet, x, torch.tensor(481), ctx)
-        t2 = time.perf_counter()
-        sd_ref.vae_decode(sds["vae"], cfg.vae, mom[:, :4])
-        t3 = time.perf_counter()
-    per_img = (t1 - t0) + n_evals * (t2 - t1) + (t3 - t2)
-    return {"value": round(1.0 / per_img, 6), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"1 image {res}x{res}: VAE encode {t1 - t0:.2f}s + 1 CFG UNet eval (batch 2) "
-                      f"{t2 - t1:.2f}s x {n_evals} + VAE decode {t3 - t2:.2f}s, fp32 PyTorch-CPU restatement "
-                      f"(oracle/sd_ref.py), {per_img:.1f}s/image extrapolated"}
+        for i in range(n_images):
+            t0 = time.perf_counter()
+            r = PR.img2img_ref(models, Image.fromarray(noisy[i]), ids_p, ids_n, strength, steps, guidance, 42, "pndm")
+            t_img.append(time.perf_counter() - t0)
+            refs.append(r)
+    per_img = float(np.mean(t_img))
+    cpu = {"value": round(1.0 / per_img, 6), "unit": "images/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+           "sample": f"BASELINE configs[0]: {n_images} full 512x512 denoise image(s), 20 PNDM steps x strength 0.5 "
+                     f"= {len(refs[0].timesteps)} UNet evals with CFG 5.0 (batch 2), VAE encode + decode, fp32 "
+                     f"PyTorch-CPU restatement (oracle/pipeline_ref.py), torch threads = usable CPUs of this "
+                     f"process ({threads}); {per_img:.1f} s/image, model load excluded"}
+
+    # the same images through the GPU engine
+    u8 = torch.from_numpy(noisy).to(device).contiguous()
+    eng32 = SDEngine(cfg, "fp32", device, state_dicts=sds)
+    g32 = eng32.img2img(u8, prompt, strength, steps, guidance, seed=42, want_float=True)
+    del eng32
+    kind = eng_bf16.cfg.scheduler.kind
+    eng_bf16.cfg.scheduler.kind = "pndm"
+    try:
+        g16 = eng_bf16.img2img(u8, prompt, strength, steps, guidance, seed=42, want_float=True)
+    finally:
+        eng_bf16.cfg.scheduler.kind = kind
+    torch.cuda.synchronize()
+    f32_max, u8_max, ps, ss, ps_gt_g, ps_gt_c, ss_gt_g, ss_gt_c = 0.0, 0, [], [], [], [], [], []
+    for i, r in enumerate(refs):
+        ref_u8 = np.asarray(r.image)
+        f32_max = max(f32_max, float(np.abs(g32.decoded01[i].cpu().numpy() - r.decoded_float).max()))
+        u8_max = max(u8_max, int(np.abs(g32.images_u8[i].cpu().numpy().astype(int) - ref_u8.astype(int)).max()))
+        b = g16.images_u8[i].cpu().numpy()
+        ps.append(M.psnr(ref_u8, b))
+        ss.append(M.ssim(ref_u8, b))
+        ps_gt_g.append(M.psnr(clean[i], b))
+        ps_gt_c.append(M.psnr(clean[i], ref_u8))
+        ss_gt_g.append(M.ssim(clean[i], b))
+        ss_gt_c.append(M.ssim(clean[i], ref_u8))
+    parity = {"workload": "BASELINE configs[0] images (512x512, 20 PNDM steps x 0.5, CFG 5.0, seed 42)",
+              "images": n_images,
+              "fp32_engine_max_abs_vs_ref": f32_max, "fp32_engine_u8_max_diff_vs_ref": u8_max,
+              "psnr_vs_ref": round(float(np.mean(ps)), 3), "ssim_vs_ref": round(float(np.mean(ss)), 5),
+              "psnr_gt": {"gpu_bf16": round(float(np.mean(ps_gt_g)), 4), "cpu_ref": round(float(np.mean(ps_gt_c)), 4)},
+              "ssim_gt": {"gpu_bf16": round(float(np.mean(ss_gt_g)), 5), "cpu_ref": round(float(np.mean(ss_gt_c)), 5)},
+              "note": "psnr/ssim_vs_ref: GPU bf16 output against the CPU fp32 reference output (metrics.py = "
+                      "skimage 0.18.3 restatement); psnr_gt / ssim_gt: both against the clean image"}
+    return cpu, parity
 
 
 def main():
@@ -121,17 +246,19 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=8, help="images per GPU")
-    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--task", default="denoise", choices=sorted(TASKS))
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's shard)")
     ap.add_argument("--sched-steps", type=int, default=50)
-    ap.add_argument("--strength", type=float, default=0.5)
-    ap.add_argument("--guidance", type=float, default=5.0)
-    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--dtype", default=None, help="bf16 | fp16 | fp32 (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-images", type=int, default=1, help="configs[0] images for the CPU baseline")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--opt", action="append", default=[], help="irx_set_option name=value (A/B experiments)")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     args = ap.parse_args()
+    spec = TASKS[args.task]
+    batch = args.batch or spec["batch"]
+    dtype = args.dtype or spec["dtype"]
+    res = spec["res"]
 
     rank, world, local = D.init()
     if world != args.gpus:
@@ -143,17 +270,22 @@ def main():
         k, v = o.split("=")
         L.call("irx_set_option", k.encode(), int(v))
 
-    cfg = PipelineConfig.default("denoise")
+    cfg = PipelineConfig.default(args.task)
     cfg.scheduler.kind = "ddim"          # BASELINE.json: "50 DDIM steps" (explicit override of the saved PNDM)
     t_init = time.perf_counter()
-    eng, sds = build_engine(cfg, args.dtype, device, rank)
-    imgs = torch.from_numpy(synthetic_batch(args.batch, args.res, seed=rank)).to(device).contiguous()
-    noise = draw_noise(42, args.res // 8, args.res // 8, 2)
-    log(f"[rank {rank}] engine ready in {time.perf_counter() - t_init:.1f}s")
+    eng, sds = build_engine(cfg, dtype, device, rank)
+    u8_h, mask_h = task_inputs(args.task, spec, batch, seed=rank)
+    imgs = torch.from_numpy(u8_h).to(device).contiguous()
+    mask = torch.from_numpy(mask_h).to(device).contiguous() if mask_h is not None else None
+    noise = draw_noise(42, res // 8, res // 8, 2)
+    prompt = PROMPTS[args.task]
+    log(f"[rank {rank}] engine ready in {time.perf_counter() - t_init:.1f}s ({args.task}, {dtype}, batch {batch})")
 
     def step():
         eng._ctx_cache.clear()              # text encoding is part of every pass
-        return eng.img2img(imgs, PROMPT, args.strength, args.sched_steps, args.guidance, seed=42, noise=noise)
+        if args.task == "inpaint":
+            return eng.inpaint(imgs, mask, prompt, spec["strength"], args.sched_steps, spec["guidance"], seed=42)
+        return eng.img2img(imgs, prompt, spec["strength"], args.sched_steps, spec["guidance"], seed=42, noise=noise)
 
     for _ in range(args.warmup):
         out = step()
@@ -168,10 +300,11 @@ def main():
     torch.cuda.synchronize()
     el = D.max_over_ranks(time.perf_counter() - t0, device)
     n_evals = len(out.timesteps)
-    images = args.batch * world * args.steps
+    finite = bool(torch.isfinite(out.latents).all().item())
+    images = batch * world * args.steps
     value = images / el
-    cfg_f = 2 if args.guidance > 1 else 1
-    tflop_img = (n_evals * cfg_f * F_UNET_512 + F_ENC_512 + F_DEC_512) / 1000.0 * (args.res / 512) ** 2
+    cfg_f = 2 if spec["guidance"] > 1 else 1
+    tflop_img = (n_evals * cfg_f * F_UNET[res] + spec["n_enc"] * F_ENC[res] + F_DEC[res]) / 1000.0
 
     roofline = None
     if not args.no_roofline:
@@ -185,38 +318,45 @@ def main():
         tot_fl = sum(p[3] for p in prof)
         prof.sort(key=lambda p: -p[2])
         if rank == 0:
-            log(f"profiled {args.steps} steps: {tot_fl / 1e12 / (args.steps * args.batch):.2f} TFLOP/img counted, "
+            log(f"profiled {args.steps} steps: {tot_fl / 1e12 / (args.steps * batch):.2f} TFLOP/img counted, "
                 f"MFMA-kernel time {tot_ms / args.steps:.1f} ms/step")
-            for name, cnt, ms, fl in prof[:18]:
+            for name, cnt, ms, fl in prof[:24]:
                 log(f"  {ms / args.steps:8.1f} ms/step {cnt // args.steps:5d} launches/step "
                     f"{fl / ms / 1e9 if ms else 0:7.1f} TF/s  {name}")
         name, cnt, ms, fl = next(p for p in prof if p[3] > 0)   # dominant MFMA kernel
-        peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+        peak = PEAK_TFLOPS[dtype]
         ach = fl / (ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": pmc_traffic(name), "kernel": name,
                     "launches": cnt, "avg_launch_us": round(ms * 1e3 / cnt, 2),
                     "flops_per_launch": fl / cnt,
-                    "all_mfma_kernels_tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 2)}
+                    "all_mfma_kernels_tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 2),
+                    "mfma_kernel_ms_per_step": round(tot_ms / args.steps, 2)}
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, sds, args.res, args.sched_steps, args.strength, args.cpu_threads)
+        if args.task != "denoise":
+            dn = PipelineConfig.default("denoise")
+            sds = {k: W.random_state_dict(k, getattr(dn, k), 0) for k in ("unet", "vae", "clip")}
+            eng = SDEngine(dn, "bf16", device, state_dicts=sds)
+        cpu, parity = cpu_baseline_and_parity(eng, sds, device, args.cpu_images, usable_cpus())
 
     if rank == 0:
         line = {
-            "metric": "restored images/sec @512x512, 50 DDIM steps",
+            "metric": "restored images/sec @512x512, 50 DDIM steps; PSNR/SSIM vs reference",
             "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-            "data": "synthetic 512x512 noisy images (sigma 5-8), seeded random SD-1.5 weights",
-            "config": {"workload": f"denoise img2img {args.res}x{args.res}, batch {args.batch}/GPU, "
-                                   f"{args.sched_steps} DDIM steps x strength {args.strength} = {n_evals} UNet evals, "
-                                   f"CFG {args.guidance} (UNet batch {args.batch * cfg_f})",
-                       "global_batch": args.batch * world, "resolution": args.res, "parallelism": f"dp{world}",
-                       "tflop_per_image": round(tflop_img, 2),
-                       "achieved_tflops_end_to_end": round(value * tflop_img, 1)},
-            "roofline": roofline, "cpu_baseline": cpu,
+            "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+            "data": f"synthetic {res}x{res} {args.task} inputs, seeded random SD-1.5 weights",
+            "config": {"workload": f"BASELINE configs[{spec['cfg'] - 1}] {args.task} {res}x{res}, batch {batch}/GPU, "
+                                   f"{args.sched_steps} DDIM steps x strength {spec['strength']} = {n_evals} UNet "
+                                   f"evals, " + (f"CFG {spec['guidance']} (UNet batch {batch * cfg_f})"
+                                                 if cfg_f == 2 else "no CFG")
+                                   + (", 9-channel UNet, 2 VAE encodes" if args.task == "inpaint" else ""),
+                       "task": args.task, "global_batch": batch * world, "resolution": res,
+                       "parallelism": f"dp{world}", "tflop_per_image": round(tflop_img, 2),
+                       "achieved_tflops_end_to_end": round(value * tflop_img, 1), "outputs_finite": finite},
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
         }
         print(json.dumps(line), flush=True)
     D.barrier()

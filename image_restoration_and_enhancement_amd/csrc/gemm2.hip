@@ -17,6 +17,7 @@
 // Requirements (else the 4-wave kernel in gemm.hip runs): bf16, K % 64 == 0, conv channel
 // counts % 64 == 0 (a 64-deep K step never straddles a tap or the concat seam).
 #include <cmath>
+#include <map>
 #include <mutex>
 
 #include "ops.h"
@@ -32,7 +33,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 constexpr int kSplitCounters = 1 << 16;
-__device__ unsigned g_splitk_cnt[kSplitCounters];   // per-(batch, tile) split arrival tickets (self-resetting)
+// Split arrival tickets live in one zero-initialised array PER STREAM (self-resetting: the last arriver
+// stores 0 back).  Launches on one stream are ordered, so a stream's tickets are never shared by two
+// GEMMs in flight; two handles on two streams get disjoint arrays (no cross-stream ticket mixing).
 
 struct Split {
   bool inkernel = false;   // last arriving split reduces (else splitk_reduce_kernel)
@@ -40,6 +43,7 @@ struct Split {
   int per = 0;         // K steps per split
   float* ws = nullptr; // fp32 partials [batch*splits][Mp][Np] (M, N rounded up to the tile: unchecked stores)
   int Mp = 0, Np = 0;
+  unsigned* cnt = nullptr;   // this stream's arrival tickets (in-kernel mode)
 };
 
 // Wait until at most n of this wave's vector-memory operations (here: LDS-DMA pieces) are outstanding.
@@ -73,7 +77,8 @@ __device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds_addr) {
 // 256x160 than the 256x320 im2col tile), with whole 128-B lines per request (BK 64).
 constexpr int kHaloWMax = 64;    // widest image row a halo tile takes (LDS: 2 x (BM + 2W) x 2BK B)
 
-template <int BM, int BN, int WM, int WN, int BK, int S, bool CONV, bool OUTF32, bool RESIZE, bool HALO = false>
+template <typename T, int BM, int BN, int WM, int WN, int BK, int S, bool CONV, bool OUTF32, bool RESIZE,
+          bool HALO = false>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kernel(GemmArgs a, Split sp) {
   constexpr int NW = WM * WN, NT = NW * 64;   // 8 waves (1 block/CU) or 4 waves (2 blocks/CU)
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
@@ -226,8 +231,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
-                                                              __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+          acc[i][j] = Mfma<T>::m16x16x32(af[i], bfr[j], acc[i][j]);
       if constexpr (S > 2) __builtin_amdgcn_s_setprio(0);
     }
   };
@@ -334,8 +338,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[ss][i]),
-                                                                  __builtin_bit_cast(bf16x8, bfr[ss][j]), acc[i][j], 0, 0, 0);
+              acc[i][j] = Mfma<T>::m16x16x32(af[ss][i], bfr[ss][j], acc[i][j]);
         __builtin_amdgcn_s_setprio(0);
       }
       st = st + 1 == S ? 0 : st + 1;
@@ -409,7 +412,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     int* flag = (int*)smem;                             // (one LDS array: no second __shared__ object)
     const int cidx = z * tiles_m * tiles_n + bid;
     if (tid == 0) {
-      const unsigned prev = __hip_atomic_fetch_add((gu32*)&g_splitk_cnt[cidx], 1u, __ATOMIC_RELAXED,
+      const unsigned prev = __hip_atomic_fetch_add((gu32*)&sp.cnt[cidx], 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
       *flag = prev == (unsigned)(sp.splits - 1);
     }
@@ -436,7 +439,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       }
     }
     if (tid == 0)   // ready for the next launch (the kernel boundary orders it)
-      __hip_atomic_store((gu32*)&g_splitk_cnt[cidx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32*)&sp.cnt[cidx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
   // ---- epilogue (D[row = 4g + r][col = lane & 15] per 16x16 tile)
@@ -464,7 +467,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = wm * TM * 16 + i * 16 + fgrp * 4 + r;
-            tileS[row * BN + (csw(col >> 3, row) << 3) + (col & 7)] = f2bf(acc[i][j][r] * a.alpha + bias);
+            tileS[row * BN + (csw(col >> 3, row) << 3) + (col & 7)] =
+                __builtin_bit_cast(uint16_t, from_f<T>(acc[i][j][r] * a.alpha + bias));
           }
       }
       __syncthreads();
@@ -478,11 +482,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           const int hc = (oc >> 3) * 16 + (oc & 7);       // value chunk; gate chunk is hc + 8
           if (m >= a.M || n0 + hc * 8 >= a.N) continue;
           float h[8], gt[8];
-          Vec16<bf16_t>::unpack(*(const uint4*)(tileS + row * BN + ((hc ^ (row & 7)) << 3)), h);
-          Vec16<bf16_t>::unpack(*(const uint4*)(tileS + row * BN + (((hc + 8) ^ (row & 7)) << 3)), gt);
+          Vec16<T>::unpack(*(const uint4*)(tileS + row * BN + ((hc ^ (row & 7)) << 3)), h);
+          Vec16<T>::unpack(*(const uint4*)(tileS + row * BN + (((hc + 8) ^ (row & 7)) << 3)), gt);
 #pragma unroll
           for (int e = 0; e < 8; ++e) h[e] = h[e] * gelu_erf(gt[e]);
-          *(uint4*)(Cp + (long)m * a.ldc + n0 / 2 + oc * 8) = Vec16<bf16_t>::pack(h);
+          *(uint4*)(Cp + (long)m * a.ldc + n0 / 2 + oc * 8) = Vec16<T>::pack(h);
         }
         return;
       }
@@ -494,7 +498,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         uint4 u = *(const uint4*)(tileS + row * BN + (csw(c, row) << 3));
         if (Rp || a.rowadd || a.out_scale != 1.f) {
           float f[8];
-          Vec16<bf16_t>::unpack(u, f);
+          Vec16<T>::unpack(u, f);
           if (a.rowadd) {   // per-image time-embedding projection (added after the bf16 rounding of pass 1)
             const float4* ra = (const float4*)(a.rowadd + (long)(m / a.rows_per_group) * a.rowadd_ld + n);
             const float4 x = ra[0], y = ra[1];
@@ -502,13 +506,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           }
           if (Rp) {
             float rv[8];
-            Vec16<bf16_t>::unpack(*(const uint4*)(Rp + (long)m * a.ldr + n), rv);
+            Vec16<T>::unpack(*(const uint4*)(Rp + (long)m * a.ldr + n), rv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] += rv[e];
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] *= a.out_scale;
-          u = Vec16<bf16_t>::pack(f);
+          u = Vec16<T>::pack(f);
         }
         *(uint4*)(Cp + (long)m * a.ldc + n) = u;
       }
@@ -528,14 +532,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         if (m >= a.M) continue;
         const float v = (acc[i][j][r] * a.alpha + bias) * a.out_scale;   // (no row add / residual here: eligible())
         if constexpr (OUTF32) ((float*)a.C)[(long)z * a.sC + (long)m * a.ldc + n] = v;
-        else ((uint16_t*)a.C)[(long)z * a.sC + (long)m * a.ldc + n] = f2bf(v);
+        else ((uint16_t*)a.C)[(long)z * a.sC + (long)m * a.ldc + n] = __builtin_bit_cast(uint16_t, from_f<T>(v));
       }
     }
   }
 }
 
 // sum of split-K partials + the full epilogue, 8 outputs (one 16-byte bf16 chunk) per thread
-template <bool OUTF32>
+template <typename T, bool OUTF32>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const float* __restrict__ ws, int splits,
                                                             int Mp, int Np) {
   const int nv = a.N / 8;
@@ -554,7 +558,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
   float rv[8];
   if (a.residual) {
     const uint16_t* R = (const uint16_t*)a.residual + (long)z * a.sR + (long)m * a.ldr + n;
-    Vec16<bf16_t>::unpack(*(const uint4*)R, rv);
+    Vec16<T>::unpack(*(const uint4*)R, rv);
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -569,42 +573,52 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
 #pragma unroll
     for (int e = 0; e < 8; ++e) C[e] = f[e];
   } else {
-    *(uint4*)((uint16_t*)a.C + (long)z * a.sC + (long)m * a.ldc + n) = Vec16<bf16_t>::pack(f);
+    *(uint4*)((uint16_t*)a.C + (long)z * a.sC + (long)m * a.ldc + n) = Vec16<T>::pack(f);
+  }
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int BK, int S, bool HALO>
+void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles, a.batch * sp.splits), block(WM * WN * 64);
+  const bool rs = a.conv && (a.g.Hv != a.g.Hin || a.g.Wv != a.g.Win);
+  const char* tn = std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short";
+  std::string nm;
+  if (prof_on())   // same spelling as the demangled name rocprofv3 reports
+    nm = std::string("irx::(anonymous namespace)::gemm2_kernel<") + tn + ", " + std::to_string(BM) + ", " +
+         std::to_string(BN) + ", " + std::to_string(WM) + ", " + std::to_string(WN) + ", " + std::to_string(BK) + ", " +
+         std::to_string(S) + ", " + (a.conv ? "true" : "false") + ", " + (a.out_f32 ? "true" : "false") + ", " +
+         (rs ? "true" : "false") + ", " + (HALO ? "true" : "false") + ">";
+  {
+    ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
+    if constexpr (HALO) {
+      gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false, true><<<grid, block, 0, s>>>(a, sp);
+    } else if (a.conv) {   // (fp32-output convs never take this path: see eligible())
+      if (rs) gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, true><<<grid, block, 0, s>>>(a, sp);
+      else gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false><<<grid, block, 0, s>>>(a, sp);
+    } else {
+      if (a.out_f32) gemm2_kernel<T, BM, BN, WM, WN, BK, S, false, true, false><<<grid, block, 0, s>>>(a, sp);
+      else gemm2_kernel<T, BM, BN, WM, WN, BK, S, false, false, false><<<grid, block, 0, s>>>(a, sp);
+    }
+    IRX_LAUNCH_CHECK();
+  }
+  if (sp.splits > 1 && !sp.inkernel) {
+    ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::splitk_reduce_kernel<") + tn + ", " +
+                                 (a.out_f32 ? "true" : "false") + ">"
+                           : std::string(),
+                 0.0, s);
+    const long n = (long)a.M * (a.N / 8);
+    dim3 g2((unsigned)((n + 255) / 256), a.batch);
+    if (a.out_f32) splitk_reduce_kernel<T, true><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits, sp.Mp, sp.Np);
+    else splitk_reduce_kernel<T, false><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits, sp.Mp, sp.Np);
+    IRX_LAUNCH_CHECK();
   }
 }
 
 template <int BM, int BN, int WM, int WN, int BK, int S, bool HALO = false>
 void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles, a.batch * sp.splits), block(WM * WN * 64);
-  const bool rs = a.conv && (a.g.Hv != a.g.Hin || a.g.Wv != a.g.Win);
-  std::string nm;
-  if (prof_on())   // same spelling as the demangled name rocprofv3 reports
-    nm = "irx::(anonymous namespace)::gemm2_kernel<" + std::to_string(BM) + ", " + std::to_string(BN) + ", " +
-         std::to_string(WM) + ", " + std::to_string(WN) + ", " + std::to_string(BK) + ", " + std::to_string(S) +
-         ", " + (a.conv ? "true" : "false") + ", " + (a.out_f32 ? "true" : "false") + ", " +
-         (rs ? "true" : "false") + ", " + (HALO ? "true" : "false") + ">";
-  {
-    ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
-    if constexpr (HALO) {
-      gemm2_kernel<BM, BN, WM, WN, BK, S, true, false, false, true><<<grid, block, 0, s>>>(a, sp);
-    } else if (a.conv) {   // (fp32-output convs never take this path: see eligible())
-      if (rs) gemm2_kernel<BM, BN, WM, WN, BK, S, true, false, true><<<grid, block, 0, s>>>(a, sp);
-      else gemm2_kernel<BM, BN, WM, WN, BK, S, true, false, false><<<grid, block, 0, s>>>(a, sp);
-    } else {
-      if (a.out_f32) gemm2_kernel<BM, BN, WM, WN, BK, S, false, true, false><<<grid, block, 0, s>>>(a, sp);
-      else gemm2_kernel<BM, BN, WM, WN, BK, S, false, false, false><<<grid, block, 0, s>>>(a, sp);
-    }
-    IRX_LAUNCH_CHECK();
-  }
-  if (sp.splits > 1 && !sp.inkernel) {
-    ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::splitk_reduce_kernel") : std::string(), 0.0, s);
-    const long n = (long)a.M * (a.N / 8);
-    dim3 g2((unsigned)((n + 255) / 256), a.batch);
-    if (a.out_f32) splitk_reduce_kernel<true><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits, sp.Mp, sp.Np);
-    else splitk_reduce_kernel<false><<<g2, 256, 0, s>>>(a, sp.ws, sp.splits, sp.Mp, sp.Np);
-    IRX_LAUNCH_CHECK();
-  }
+  if (a.dtype == F16) launch2_t<f16_t, BM, BN, WM, WN, BK, S, HALO>(a, sp, s);
+  else launch2_t<bf16_t, BM, BN, WM, WN, BK, S, HALO>(a, sp, s);
 }
 
 // ------------------------------------------------------------------ tile / split policy
@@ -677,6 +691,18 @@ Choice choose(const GemmArgs& a) {
 }
 
 std::mutex g_ws_mu;
+std::map<hipStream_t, unsigned*> g_cnt;   // per-stream split-K tickets (never freed: 256 KiB per stream)
+
+unsigned* stream_counters(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  auto it = g_cnt.find(s);
+  if (it != g_cnt.end()) return it->second;
+  unsigned* p = nullptr;
+  IRX_HIP(hipMalloc(&p, kSplitCounters * sizeof(unsigned)));
+  IRX_HIP(hipMemset(p, 0, kSplitCounters * sizeof(unsigned)));   // synchronous: zero before any launch uses it
+  g_cnt[s] = p;
+  return p;
+}
 float* g_ws = nullptr;
 size_t g_ws_bytes = 0;
 
@@ -703,7 +729,7 @@ bool eligible(const GemmArgs& a) {
   // the unrolled scalar (non-16-byte) epilogue only scales and adds bias: row add / residual need vec rows
   if (!vec_ok(a) && (a.rowadd || a.residual)) return false;
   if (a.rowadd && (a.rowadd_ld % 4 != 0 || ((uintptr_t)a.rowadd % 16) != 0)) return false;
-  if (a.dtype != BF16 || a.K % bk != 0 || a.ldb % 8 != 0) return false;
+  if (!is16(a.dtype) || a.K % bk != 0 || a.ldb % 8 != 0) return false;
   if ((long)a.M * a.batch < 512) return false;     // tiny outputs: the 64x64 4-wave tiles waste less
   if (a.geglu && (a.out_f32 || a.residual || a.batch != 1 || a.N % 128 != 0)) return false;
   if (a.conv) return !a.out_f32 && a.g.C0 % bk == 0 && a.g.C1 % bk == 0;
@@ -785,6 +811,7 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     const long tiles = (long)((a.M + c.BM - 1) / c.BM) * ((a.N + c.BN - 1) / c.BN) * a.batch;
     // in-kernel reduction wins at 2 splits; with more, the serial last-arriver tail loses to the reduce kernel
     sp.inkernel = g_splitk_inkernel && c.splits == 2 && tiles <= kSplitCounters;
+    if (sp.inkernel) sp.cnt = stream_counters(s);
   } else {
     sp.per = a.K / step_k();
   }

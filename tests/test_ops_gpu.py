@@ -374,3 +374,26 @@ def test_attention_d40_variants(device, variant, B, Lq, Lk):
         L.call("irx_set_option", b"attn_d40", 2)
     ref = O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), 8)
     assert O.rel_err(got, ref) < 2 * TOL[dt]
+
+
+def test_gemm_splitk_two_streams(device):
+    """Two streams running in-kernel split-K GEMMs concurrently (the arrival tickets were one
+    process-global array): each stream's results equal a single-stream run bit for bit."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    dt = torch.bfloat16
+    shapes = [(4096, 1280, 1280), (1024, 1280, 2560)]
+    ins = [(_dev(_r(M, K, seed=94 + i), dt, device), _dev(_r(N, K, seed=96 + i, scale=1 / math.sqrt(K)), dt, device))
+           for i, (M, N, K) in enumerate(shapes)]
+    L.call("irx_set_option", b"splitk_inkernel", 1)
+    want = [O.gemm(a, b) for a, b in ins]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [[], []]
+    for _ in range(8):
+        for i, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                outs[i].append(O.gemm(*ins[i]))
+    torch.cuda.synchronize()
+    for i in range(2):
+        for o in outs[i]:
+            assert torch.equal(o, want[i])
