@@ -12,7 +12,7 @@ from pathlib import Path
 _PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("IRX_LIB", _PKG / "libirx.so"))
 
-IRX_F32, IRX_BF16 = 0, 1
+IRX_F32, IRX_BF16, IRX_F16 = 0, 1, 2
 IRX_MODEL_UNET, IRX_MODEL_VAE, IRX_MODEL_CLIP = 0, 1, 2
 IRX_LAYOUT_VEC, IRX_LAYOUT_MAT, IRX_LAYOUT_CONV, IRX_LAYOUT_EMB = 0, 1, 2, 3
 IRX_LAYOUT_MAT_GEGLU64, IRX_LAYOUT_VEC_GEGLU64 = 4, 5
@@ -37,7 +37,8 @@ class ModelConfig(C.Structure):
 
 class ParamInfo(C.Structure):
     _fields_ = [("name", C.c_char_p), ("layout", C.c_int), ("dtype", C.c_int), ("ndim", C.c_int),
-                ("shape", C.c_int64 * 4), ("offset", C.c_size_t), ("bytes", C.c_size_t)]
+                ("shape", C.c_int64 * 4), ("offset", C.c_size_t), ("bytes", C.c_size_t),
+                ("row_scale", C.c_float), ("scale_rows", C.c_int64)]
 
 
 class StepParams(C.Structure):
@@ -109,6 +110,7 @@ _SIGS = {
     "irx_op_layer_norm": (i32, [vp, i32, vp, i32, i32, f32, vp, vp, vp]),
     "irx_op_attention": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp,
                                i64, i64, f32, i32]),
+    "irx_op_attention_hm": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32]),
     "irx_op_geglu": (i32, [vp, i32, vp, i32, i32, vp]),
     "irx_op_gemm_geglu": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, vp]),
 }

@@ -22,9 +22,12 @@ LIB = PKG / "libirx.so"
 ARCH = os.environ.get("IRX_OFFLOAD_ARCH", "gfx950")
 BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
               "-Wno-unused-variable", "-Wno-unused-but-set-variable", f"-I{INCLUDE}"]
+# -ffp-contract=off where a kernel must match a numpy / fp32 restatement operation for operation (no FMA
+# fusion); attention: fmaxf without NaN-quieting canonicalisations
 PER_FILE = {"elementwise.hip": ["-ffp-contract=off"],
             "attention.hip": ["-fno-honor-nans"],
-            "filters.hip": ["-ffp-contract=off"]}   # fmaxf without NaN-quieting canonicalisations
+            "filters.hip": ["-ffp-contract=off"],
+            "degrade.hip": ["-ffp-contract=off"]}
 
 
 def _hipcc() -> str:

@@ -45,9 +45,9 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
   const int q0 = qb0 + wave * (kQT * 16);
   const int d = a.d;
 
-  const T* __restrict__ Q = (const T*)a.q + (long)b * a.sq + (long)h * d;
-  const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * d;
-  const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * d;
+  const T* __restrict__ Q = (const T*)a.q + (long)b * a.sq + (long)h * (a.hsq ? a.hsq : d);
+  const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : d);
+  const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : d);
 
   // zero the padded LDS columns once (loads only ever write columns < d)
   for (int i = tid; i < kKT * SK; i += 256) Ks[i] = T(0);
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
 #pragma unroll
   for (int j = 0; j < kQT; ++j) { mrow[j] = -INFINITY; lrow[j] = 0.f; }
 
-  const float sl2 = a.scale * 1.4426950408889634f;   // softmax in base 2: exp(x*scale) = exp2(x*sl2)
+  const float sl2 = a.q_scaled ? 1.f : a.scale * 1.4426950408889634f;   // softmax in base 2: exp(x*scale) = exp2(x*sl2)
   int kend = a.Lk;
   if (a.causal) kend = min(kend, qb0 + kQB);
   const int cpr = d * (int)sizeof(T) / 16;           // 16-byte chunks per K/V row
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
   }
 
   // ---- normalise and store O[q][h*d + e]
-  T* __restrict__ O = (T*)a.o + (long)b * a.so + (long)h * d;
+  T* __restrict__ O = (T*)a.o + (long)b * a.so + (long)h * (a.hso ? a.hso : d);
 #pragma unroll
   for (int qt = 0; qt < kQT; ++qt) {
     float l = lrow[qt];
@@ -320,9 +320,9 @@ __global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
   const int qb0 = blockIdx.x * kQB;
   const int q0 = qb0 + wave * (kQT * 16);
   const int d = a.d;
-  const bf16_t* __restrict__ Q = (const bf16_t*)a.q + (long)b * a.sq + (long)h * d;
-  const bf16_t* __restrict__ K = (const bf16_t*)a.k + (long)b * a.sk + (long)h * d;
-  const bf16_t* __restrict__ V = (const bf16_t*)a.v + (long)b * a.sv + (long)h * d;
+  const bf16_t* __restrict__ Q = (const bf16_t*)a.q + (long)b * a.sq + (long)h * (a.hsq ? a.hsq : d);
+  const bf16_t* __restrict__ K = (const bf16_t*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : d);
+  const bf16_t* __restrict__ V = (const bf16_t*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : d);
 
   for (int i = tid; i < KT * SK; i += 256) Ks[i] = 0;
   for (int i = tid; i < KT * SV; i += 256) Vs[i] = (ONES && i % SV == a.d) ? (bf16_t)0x3F80 : (bf16_t)0;
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
 #pragma unroll
   for (int j = 0; j < kQT; ++j) { mrow[j] = -INFINITY; lrow[j] = 0.f; }
 
-  const float sl2 = a.scale * 1.4426950408889634f;
+  const float sl2 = a.q_scaled ? 1.f : a.scale * 1.4426950408889634f;
   int kend = a.Lk;
   if (a.causal) kend = min(kend, qb0 + kQB);
   const int cpr = d / 8;                                   // 16-byte chunks per K/V row
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
     }
   }
 
-  bf16_t* __restrict__ O = (bf16_t*)a.o + (long)b * a.so + (long)h * d;
+  bf16_t* __restrict__ O = (bf16_t*)a.o + (long)b * a.so + (long)h * (a.hso ? a.hso : d);
 #pragma unroll
   for (int qt = 0; qt < kQT; ++qt) {
     float l;
@@ -504,6 +504,283 @@ __global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
       for (int i = 0; i < 4; ++i) v[i] = (short)f2bf(o[dt][qt][i] * inv);
       *(s16x4*)(O + (long)q * a.ldo + e) = v;
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// attn3: bf16 / fp16 flash attention on v_mfma_f32_32x32x16 (the shape that holds the SIMD's VALU issue
+// for 8 of its 32 cycles instead of 8 of 16 — this kernel is bounded by the softmax VALU work at d = 40).
+//   S^T = K Q^T per 32-key sub-tile: A = K rows (ds_read_b128), B = Q^T in registers (d padded to 16);
+//     lane = query column (lane & 31), its 16 accumulator registers = 16 of the 32 keys, the other 16 in
+//     lane ^ 32 (one v_permlane32_swap finishes a row max).
+//   P^T is that accumulator converted in place: registers 8s .. 8s+7 are the B operand of k-step s of
+//     O^T += V^T P^T (guide §3, "an accumulator tile as the next MFMA's operand"); the V^T A operand comes
+//     out of the row-major V tile with two ds_read_b64_tr_b16 per k-step, in the matching key order.
+//   Softmax in base 2 with scale*log2(e) folded into q (in the to_q weights, or here at the Q load) and
+//     the running max folded into the accumulator initialisation: S' = Q K^T - m comes out of the MFMA
+//     chain and p = exp2(S') needs no subtraction.  The max is deferred (guide T13): m moves only when a
+//     tile's max exceeds it by more than THR = 8, so p <= 2^8 (exact in bf16/fp16 storage; row sums and
+//     O in fp32).  At a move, the pending tile's S' and everything accumulated (O, row sum) are rescaled
+//     once, before any of this tile's p is formed.
+//   Row sums: a ones column at V column d (d % 32 != 0 leaves a zero pad column) makes the PV MFMAs
+//     produce sum_k p (the same rounded p as the numerator); d % 32 == 0: fp32 VALU sums.
+// Block = 4 waves x 32 queries; KT = 64 keys per tile, register-staged K/V prefetch.  Grid: (batch, head) groups of query blocks on one XCD.
+template <typename T> constexpr uint16_t one_bits();
+template <> constexpr uint16_t one_bits<bf16_t>() { return 0x3F80; }
+template <> constexpr uint16_t one_bits<f16_t>() { return 0x3C00; }
+
+__device__ __forceinline__ float xlane32(float x) {   // value of lane l ^ 32
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? b[0] : b[1]);
+}
+
+// waves per SIMD the register file allows without spills (d = 40 / 64-key tiles is the hot instantiation)
+template <int D, int KT> constexpr int attn3_occ() {
+  return D <= 40 ? (KT <= 64 ? 4 : 3) : D <= 64 ? (KT <= 64 ? 3 : 2) : D <= 80 ? 2 : 1;
+}
+
+template <typename T, int D, int KT, bool CAUSAL>
+__global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnArgs a) {
+  constexpr int QB = 128;                                  // queries per block (4 waves x 32)
+  constexpr int DQ = (D + 15) / 16 * 16, NS = DQ / 16;     // QK^T contraction, 16-deep k-steps
+  constexpr int NDT = (D + 31) / 32;                       // 32-row tiles of O^T
+  constexpr bool ONES = D % 32 != 0;
+  constexpr int DVP = NDT * 32;
+  constexpr int SK = ((DQ / 8) % 2 == 0) ? DQ + 8 : DQ;   // odd 16-B slots per row: b128 reads conflict-free
+  constexpr int SV = (DVP % 128 == 32 || DVP % 128 == 96) ? DVP : DVP + 32;   // tr reads conflict-free
+  constexpr int NSUB = KT / 32;
+  constexpr int CPR = D / 8;                               // 16-byte chunks per K/V row
+  constexpr int NCH = (KT * CPR + 255) / 256;
+  constexpr float THR = 8.f;
+  static_assert(D % 8 == 0 && KT % 32 == 0, "attn3 shape");
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[KT * SK];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[KT * SV];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5, g = lane >> 4;
+  const int nq = (a.Lq + QB - 1) / QB;
+  const int nblk = nq * a.H * a.B;
+  const int lid = a.xcd ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
+  const int qb = lid % nq, bh = lid / nq;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int q0 = qb * QB + wave * 32;
+  const int qrow = q0 + r;
+  const T* __restrict__ Q = (const T*)a.q + (long)b * a.sq + (long)h * (a.hsq ? a.hsq : D);
+  const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : D);
+  const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : D);
+
+  for (int i = tid; i < KT * SK; i += 256) Ks[i] = 0;
+  for (int i = tid; i < KT * SV; i += 256) Vs[i] = (ONES && i % SV == D) ? one_bits<T>() : (uint16_t)0;
+
+  // Q^T fragments (B operand): lane (r, hh) holds q[qrow][16s + 8hh .. +7], pre-scaled by scale*log2(e)
+  uint4 qf[NS];
+  const float sl2 = a.scale * 1.4426950408889634f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int e = 16 * s + 8 * hh;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (qrow < a.Lq && e < D) v = *(const uint4*)(Q + (long)qrow * a.ldq + e);
+    if (!a.q_scaled) {
+      float f[8];
+      Vec16<T>::unpack(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= sl2;
+      v = Vec16<T>::pack(f);
+    }
+    qf[s] = v;
+  }
+
+  f32x16 oacc[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) oacc[i][k] = 0.f;
+  // m: the running max, always a value of the storage type (so -m is exact in a 16-bit operand).
+  // PADM (d < the 16-padded contraction): -m rides in the zero padding as one more k: K[.][d] = 1 (in LDS),
+  // Q[q][d] = -m (lane half 1, k-step NS-1, element 0), so the MFMA chain itself yields S - m.  Otherwise
+  // the accumulators start at -m.
+  constexpr bool PADM = DQ > D;
+  constexpr int PADS = D / 16, PADE = (D % 16) - 8;   // k-step and element of column d in lane half 1
+  static_assert(!PADM || (D % 16 == 8 && PADE == 0), "pad column at element 0 of lane half 1");
+  float m = 0.f, lsum = 0.f;
+  bool first = true;
+  auto set_qpad = [&]() {   // Q^T fragment element holding -m (lane half 1 only; lane half 0 holds d-8 .. d-1)
+    if constexpr (PADM) {
+      if (hh) qf[PADS].x = (qf[PADS].x & 0xFFFF0000u) | (Mfma<T>::pack2(-m, 0.f) & 0xFFFFu);
+    }
+  };
+  if constexpr (PADM)
+    for (int i = tid; i < KT; i += 256) Ks[i * SK + D] = one_bits<T>();
+
+  const int kend = CAUSAL ? min(a.Lk, qb * QB + QB) : a.Lk;
+  uint4 kreg[NCH], vreg[NCH];
+  auto load = [&](int j0) {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = tid + 256 * u;
+      kreg[u] = make_uint4(0, 0, 0, 0);
+      vreg[u] = make_uint4(0, 0, 0, 0);
+      if (idx < KT * CPR) {
+        const int row = idx / CPR, c = idx - row * CPR;
+        if (j0 + row < a.Lk) {
+          kreg[u] = *(const uint4*)(K + (long)(j0 + row) * a.ldk + c * 8);
+          vreg[u] = *(const uint4*)(V + (long)(j0 + row) * a.ldv + c * 8);
+        }
+      }
+    }
+  };
+  load(0);
+
+  for (int j0 = 0; j0 < kend; j0 += KT) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = tid + 256 * u;
+      if (idx < KT * CPR) {
+        const int row = idx / CPR, c = idx - row * CPR;
+        *(uint4*)(Ks + row * SK + c * 8) = kreg[u];
+        *(uint4*)(Vs + row * SV + c * 8) = vreg[u];
+      }
+    }
+    __syncthreads();
+    if (j0 + KT < kend) load(j0 + KT);
+
+    // ---- S'^T = K Q^T - m
+    f32x16 sacc[NSUB];
+    const float init = (PADM || first) ? 0.f : -m;
+#pragma unroll
+    for (int c = 0; c < NSUB; ++c)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sacc[c][k] = init;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int c = 0; c < NSUB; ++c) {
+        const uint4 kf = *(const uint4*)(Ks + (c * 32 + r) * SK + 16 * s + 8 * hh);
+        sacc[c] = Mfma<T>::m32x32x16(kf, qf[s], sacc[c]);
+      }
+    if (j0 + KT > a.Lk || (CAUSAL && j0 + KT - 1 > q0)) {
+#pragma unroll
+      for (int c = 0; c < NSUB; ++c)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int key = j0 + 32 * c + (k & 3) + 8 * (k >> 2) + 4 * hh;
+          if (key >= a.Lk || (CAUSAL && key > qrow)) sacc[c][k] = -INFINITY;
+        }
+    }
+    // row max: 3-input max chains (v_max3_f32), then the other lane half
+    float tmax = fmaxf(sacc[0][0], sacc[0][1]);
+#pragma unroll
+    for (int c = 0; c < NSUB; ++c)
+#pragma unroll
+      for (int k = (c == 0 ? 2 : 0); k < 16; k += 2) tmax = fmaxf(fmaxf(tmax, sacc[c][k]), sacc[c][k + 1]);
+    tmax = fmaxf(tmax, xlane32(tmax));
+    if (first || __any(tmax > THR)) {
+      // move m (first tile: to the tile max; later: up by the excess, deferred until it passes THR)
+      const float tgt = first ? (tmax == -INFINITY ? 0.f : m + tmax) : m + fmaxf(tmax, 0.f);
+      const float mn = Mfma<T>::round(tgt);
+      const float delta = mn - m;
+      const float alpha = __builtin_amdgcn_exp2f(-delta);
+#pragma unroll
+      for (int c = 0; c < NSUB; ++c)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sacc[c][k] -= delta;
+      if (!first) {
+#pragma unroll
+        for (int i = 0; i < NDT; ++i)
+#pragma unroll
+          for (int k = 0; k < 16; ++k) oacc[i][k] *= alpha;
+        if constexpr (!ONES) lsum *= alpha;
+      }
+      m = mn;
+      first = false;
+      set_qpad();
+    }
+
+    // ---- O^T += V^T P^T, one 32-key sub-tile at a time
+#pragma unroll
+    for (int c = 0; c < NSUB; ++c) {
+      uint4 pb[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          p[j] = __builtin_amdgcn_exp2f(sacc[c][8 * s2 + j]);
+          if constexpr (!ONES) lsum += p[j];
+        }
+        pb[s2] = make_uint4(Mfma<T>::pack2(p[0], p[1]), Mfma<T>::pack2(p[2], p[3]), Mfma<T>::pack2(p[4], p[5]),
+                            Mfma<T>::pack2(p[6], p[7]));
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int krow = 32 * c + 16 * s2 + 4 * (g >> 1) + ((lane & 15) >> 2);
+          const int col = 32 * dt + 16 * (g & 1) + 4 * (lane & 3);
+          const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + krow * SV + col));
+          const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + (krow + 8) * SV + col));
+          const uint4 vf = make_uint4(__builtin_bit_cast(uint2, t1).x, __builtin_bit_cast(uint2, t1).y,
+                                      __builtin_bit_cast(uint2, t2).x, __builtin_bit_cast(uint2, t2).y);
+          oacc[dt] = Mfma<T>::m32x32x16(vf, pb[s2], oacc[dt]);
+        }
+    }
+  }
+
+  // ---- normalise, store O[q][h*d + e] (runs of 4 consecutive e per lane)
+  float l;
+  if constexpr (ONES) {
+    constexpr int dts = D / 32, rho = D % 32, hs = (rho >> 2) & 1, reg = (rho & 3) + 4 * (rho >> 3);
+    const float v = oacc[dts][reg];
+    const float o = xlane32(v);
+    l = hh == hs ? v : o;
+  } else {
+    l = lsum + xlane32(lsum);
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (qrow >= a.Lq) return;
+  T* __restrict__ O = (T*)a.o + (long)b * a.so + (long)h * (a.hso ? a.hso : D) + (long)qrow * a.ldo;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = 32 * dt + 8 * k + 4 * hh;
+      if (e >= D) continue;
+      *(uint2*)(O + e) = make_uint2(Mfma<T>::pack2(oacc[dt][4 * k] * inv, oacc[dt][4 * k + 1] * inv),
+                                    Mfma<T>::pack2(oacc[dt][4 * k + 2] * inv, oacc[dt][4 * k + 3] * inv));
+    }
+}
+
+template <typename T, int D, int KT, bool CAUSAL>
+void launch3_cfg(const AttnArgs& a, hipStream_t s) {
+  const int nq = (a.Lq + 127) / 128;
+  dim3 grid(nq * a.H * a.B), block(256);
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn3_kernel<") +
+                               (std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short") + ", " +
+                               std::to_string(D) + ", " + std::to_string(KT) + ", " + (CAUSAL ? "true" : "false") + ">"
+                         : std::string(),
+               4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
+  AttnArgs b = a;
+  b.xcd = g_attn_xcd;
+  attn3_kernel<T, D, KT, CAUSAL><<<grid, block, 0, s>>>(b);
+  IRX_LAUNCH_CHECK();
+}
+
+template <typename T, int D>
+void launch3_d(const AttnArgs& a, hipStream_t s) {
+  // (96-key single-pass tiles for Lk <= 96 spill at every d: 64-key tiles everywhere, Lk = 77 in two)
+  if (a.causal) launch3_cfg<T, D, 64, true>(a, s);
+  else launch3_cfg<T, D, 64, false>(a, s);
+}
+
+template <typename T>
+bool launch3(const AttnArgs& a, hipStream_t s) {
+  switch (a.d) {
+    case 40: launch3_d<T, 40>(a, s); return true;
+    case 64: launch3_d<T, 64>(a, s); return true;
+    case 80: launch3_d<T, 80>(a, s); return true;
+    case 160: launch3_d<T, 160>(a, s); return true;
+    default: return false;
   }
 }
 
@@ -561,10 +838,17 @@ void attention(const AttnArgs& a, hipStream_t s) {
   IRX_CHECK((a.ldk * es) % 16 == 0 && (a.ldv * es) % 16 == 0, "K/V rows must be 16-byte aligned");
   IRX_CHECK((a.ldq * es) % 8 == 0 && (a.ldo * es) % 8 == 0, "Q/O rows must be 8-byte aligned");
   IRX_CHECK(((uintptr_t)a.k % 16) == 0 && ((uintptr_t)a.v % 16) == 0, "K/V base alignment");
+  const bool v16 = a.d % 8 == 0 && (a.ldq % 8) == 0 && ((uintptr_t)a.q % 16) == 0 && ((uintptr_t)a.o % 8) == 0 &&
+                   (a.ldo % 4) == 0;
   if (a.dtype == F32) launch_t<float>(a, s);
-  else if (g_attn_v2 && a.d % 8 == 0 && (a.ldq % 8) == 0 && ((uintptr_t)a.q % 16) == 0) launch_bf16(a, s);
+  else if (a.dtype == F16) {
+    IRX_CHECK(v16 && launch3<f16_t>(a, s), "fp16 attention: head dim must be 40 / 64 / 80 / 160 with 16-byte rows");
+  } else if (g_attn_v3 && v16 && launch3<bf16_t>(a, s)) {
+  } else if (g_attn_v2 && v16) launch_bf16(a, s);
   else launch_t<bf16_t>(a, s);
 }
+int g_attn_v3 = 1;
+int g_attn_xcd = 1;
 
 bool g_attn_v2 = true;
 int g_attn_d40 = 2;   // d = 40 variant (A/B): 0 128-key tiles (ones-column row sums), 1 VALU row sums,

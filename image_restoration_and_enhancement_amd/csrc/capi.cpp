@@ -70,6 +70,8 @@ int irx_set_option(const char* name, int value) {
   else if (n == "conv_halo") g_conv_halo = value;
   else if (n == "gemm_small") g_gemm_small = value != 0;
   else if (n == "attn_d40") g_attn_d40 = value;
+  else if (n == "attn_v3") g_attn_v3 = value;
+  else if (n == "attn_xcd") g_attn_xcd = value;
   else if (n == "gemm_small_kmax") g_gemm_small_kmax = value;
   else if (n == "nlm_strip") g_nlm_strip = value;
   else if (n == "nlm_v2") g_nlm_v2 = value;
@@ -99,7 +101,7 @@ int irx_profile_get(int i, const char** name, long* launches, double* ms, double
 int irx_model_create(int kind, const irx_model_config* cfg, int dtype, irx_model** out) {
   IRX_API_BEGIN
   IRX_CHECK(cfg && out, "null argument");
-  IRX_CHECK(dtype == IRX_F32 || dtype == IRX_BF16, "dtype must be IRX_F32 or IRX_BF16");
+  IRX_CHECK(dtype == IRX_F32 || dtype == IRX_BF16 || dtype == IRX_F16, "dtype must be IRX_F32, IRX_BF16 or IRX_F16");
   auto* h = new irx_model;
   try {
     if (kind == IRX_MODEL_UNET) h->m.reset(new Unet(*cfg, dtype));
@@ -140,6 +142,8 @@ int irx_model_param_info(const irx_model* m, int i, irx_param_info* info) {
   for (int k = 0; k < 4; ++k) info->shape[k] = k < info->ndim ? e.shape[k] : 1;
   info->offset = e.off;
   info->bytes = e.bytes;
+  info->row_scale = e.row_scale;
+  info->scale_rows = e.scale_rows;
   IRX_API_END
 }
 
@@ -308,6 +312,7 @@ int irx_degrade_strokes(void* s, int batch, int H, int W, const int* segs, const
                         uint8_t* mask, const uint8_t* img, uint8_t* masked) {
   IRX_API_BEGIN
   IRX_CHECK(seg_off && mask && batch >= 0 && H > 0 && W > 0, "bad arguments");
+  IRX_CHECK(H <= (1 << 14) && W <= (1 << 14), "stroke masks: H, W <= 16384 (exact int64 capsule test)");
   if (batch) degrade_strokes(batch, H, W, segs, thick, seg_off, mask, img, masked, S(s));
   IRX_API_END
 }
@@ -485,6 +490,20 @@ int irx_op_attention(void* s, int dtype, int B, int H, int lq, int lk, int d, co
   a.v = v; a.ldv = ldv; a.sv = sv;
   a.o = o; a.ldo = ldo; a.so = so;
   a.scale = scale; a.causal = causal;
+  attention(a, S(s));
+  IRX_API_END
+}
+
+int irx_op_attention_hm(void* s, int dtype, int B, int H, int lq, int lk, int d, const void* q, const void* k,
+                        const void* v, void* o, float scale) {
+  IRX_API_BEGIN
+  AttnArgs a;
+  a.dtype = dtype; a.B = B; a.H = H; a.Lq = lq; a.Lk = lk; a.d = d;
+  a.q = q; a.ldq = d; a.sq = (long)H * lq * d; a.hsq = (long)lq * d;
+  a.k = k; a.ldk = d; a.sk = (long)H * lk * d; a.hsk = (long)lk * d;
+  a.v = v; a.ldv = d; a.sv = (long)H * lk * d; a.hsv = (long)lk * d;
+  a.o = o; a.ldo = d; a.so = (long)H * lq * d; a.hso = (long)lq * d;
+  a.scale = scale;
   attention(a, S(s));
   IRX_API_END
 }

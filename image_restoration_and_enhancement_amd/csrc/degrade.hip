@@ -174,17 +174,18 @@ __global__ __launch_bounds__(256) void gray_kernel(const uint8_t* __restrict__ i
 // test against that short list only.
 constexpr int kStrokeT = 16, kStrokeMaxList = 1024;
 __device__ __forceinline__ bool in_capsule(int x, int y, const int* sg, int t) {
-  // integer coordinates < 2^15: every product below is an integer < 2^53, exact in fp64 (and far cheaper
-  // than 64-bit integer multiplies)
-  const double x0 = sg[0], y0 = sg[1], x1 = sg[2], y1 = sg[3], tt = (double)t * t;
-  const double dx = x1 - x0, dy = y1 - y0, vx = x - x0, vy = y - y0;
-  const double L2 = dx * dx + dy * dy, dot = vx * dx + vy * dy;
-  if (L2 == 0.0 || dot <= 0.0) return 4.0 * (vx * vx + vy * vy) <= tt;
+  // int64 throughout, as the numpy oracle (oracle/degrade_ref.py stroke_mask): exact while every coordinate
+  // lies in [-2^15, 2^15) — then (vx^2 + vy^2) * L2 < 2^62 (irx_degrade_strokes checks H, W <= 2^14; the
+  // stroke generator clips its points to the image)
+  const long x0 = sg[0], y0 = sg[1], x1 = sg[2], y1 = sg[3], tt = (long)t * t;
+  const long dx = x1 - x0, dy = y1 - y0, vx = x - x0, vy = y - y0;
+  const long L2 = dx * dx + dy * dy, dot = vx * dx + vy * dy;
+  if (L2 == 0 || dot <= 0) return 4 * (vx * vx + vy * vy) <= tt;
   if (dot >= L2) {
-    const double ux = x - x1, uy = y - y1;
-    return 4.0 * (ux * ux + uy * uy) <= tt;
+    const long ux = x - x1, uy = y - y1;
+    return 4 * (ux * ux + uy * uy) <= tt;
   }
-  return 4.0 * ((vx * vx + vy * vy) * L2 - dot * dot) <= tt * L2;   // perpendicular distance^2 * L2
+  return 4 * ((vx * vx + vy * vy) * L2 - dot * dot) <= tt * L2;   // perpendicular distance^2 * L2
 }
 
 __global__ __launch_bounds__(256) void stroke_kernel(int B, int H, int W, const int* __restrict__ segs,

@@ -256,6 +256,9 @@ __global__ void scale_copy_kernel(const float* __restrict__ in, long npix, float
     if ((dtype) == F32) {                      \
       using T = float;                         \
       KERNEL_CALL;                             \
+    } else if ((dtype) == F16) {               \
+      using T = f16_t;                         \
+      KERNEL_CALL;                             \
     } else {                                   \
       using T = bf16_t;                        \
       KERNEL_CALL;                             \

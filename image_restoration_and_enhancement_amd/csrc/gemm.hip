@@ -181,9 +181,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           if constexpr (sizeof(T) == 2) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
-                                                                __builtin_bit_cast(bf16x8, bfr[j]),
-                                                                acc[i][j], 0, 0, 0);
+            acc[i][j] = Mfma<T>::m16x16x32(af[i], bfr[j], acc[i][j]);
           } else {
             // lane group g holds k = 16s + 4g + e in component e: four K=4 MFMAs cover the 16-deep slice
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i].x), __uint_as_float(bfr[j].x), acc[i][j], 0, 0, 0);
@@ -225,7 +223,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs a) {
 // kernel instantiation name as rocprofv3 prints it (demangled), used by the in-process profiler
 template <typename T, int WM, int WN, int TM, int TN>
 std::string kname(bool conv, bool f32out) {
-  return std::string("irx::(anonymous namespace)::gemm_kernel<") + (sizeof(T) == 2 ? "unsigned short" : "float") +
+  return std::string("irx::(anonymous namespace)::gemm_kernel<") + (sizeof(T) == 4 ? "float" : std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short") +
          ", " + std::to_string(WM) + ", " + std::to_string(WN) + ", " + std::to_string(TM) + ", " +
          std::to_string(TN) + ", " + (conv ? "true" : "false") + ", " + (f32out ? "true" : "false") + ">";
 }
@@ -281,7 +279,9 @@ void gemm(const GemmArgs& a, hipStream_t s) {
     return;
   }
   if (a.dtype == F32) launch_t<float>(a, s);
-  else if (!(g_large_tiles && gemm_large_tile(a, s))) launch_t<bf16_t>(a, s);
+  else if (g_large_tiles && gemm_large_tile(a, s)) return;
+  else if (a.dtype == F16) launch_t<f16_t>(a, s);
+  else launch_t<bf16_t>(a, s);
 }
 
 }  // namespace irx

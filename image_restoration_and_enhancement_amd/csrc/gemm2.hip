@@ -632,6 +632,13 @@ struct Choice {
 
 int step_k() { return g_gemm_deep == 1 ? 32 : 64; }   // K depth of one pipeline stage
 
+// rows (M x batch) the policy plans for: image-indexed GEMMs at kCanonImages images (batch invariance)
+long canon_rows(const GemmArgs& a) {
+  const long rows = (long)a.M * a.batch;
+  return a.imgs > 0 ? rows / a.imgs * kCanonImages : rows;
+}
+int canon_batch(const GemmArgs& a) { return (a.imgs > 0 && a.batch > 1) ? kCanonImages : a.batch; }
+
 Choice choose(const GemmArgs& a) {
   Choice best;
   const int nk = a.K / step_k();
@@ -645,7 +652,7 @@ Choice choose(const GemmArgs& a) {
   if (g_gemm_force > 0 && g_gemm_deep == 0) {   // tuning sweeps: BM*100000 + BN*100 + splits
     const int BM = g_gemm_force / 100000, BN = (g_gemm_force / 100) % 1000, sp = g_gemm_force % 100;
     const bool ok = (BM == 256 || BM == 128) && (BN == 320 || BN == 256 || BN == 128) && a.N % BN == 0 &&
-                    sp >= 1 && (sp == 1 || !((a.out_f32 && a.batch > 1) || a.geglu)) && (!a.geglu || BN % 128 == 0) &&
+                    sp >= 1 && (sp == 1 || !((a.out_f32 && canon_batch(a) > 1) || a.geglu)) && (!a.geglu || BN % 128 == 0) &&
                     !(BM == 256 && BN == 128);   // (256x128 is a 4x2-wave shape: not forced)
     if (ok) {
       best.BM = BM; best.BN = BN; best.splits = sp; best.per = (nk + sp - 1) / sp;
@@ -661,7 +668,7 @@ Choice choose(const GemmArgs& a) {
     if (BN == 320 && BM == 256 && (g_gemm_deep != 0 || !g_tile_256x320)) continue;
     if (a.N % BN != 0) continue;
     if (a.geglu && BN % 128 != 0) continue;      // tiles must hold whole (value, gate) block pairs
-    const long tiles = (long)((a.M + BM - 1) / BM) * (a.N / BN) * a.batch;
+    const long tiles = (canon_rows(a) + BM - 1) / BM * (a.N / BN);
     // per-tile efficiency at full occupancy, calibrated on the batch-16 UNet / batch-8 VAE shapes
     // (scripts/gemm_sweep.py): the load path (L2 -> LDS-DMA) bounds the small tiles, 128x128 keeps two
     // blocks per CU resident (its prologue / epilogue overlap the other block's loop), 256x128 (4x2 waves)
@@ -671,7 +678,7 @@ Choice choose(const GemmArgs& a) {
     const int resident = (BM == 128 && BN == 128 && g_gemm_deep == 0) ? 2 : 1;
     const long cap = (long)kCUs * resident;
     for (int splits = 1; splits <= 8; splits *= 2) {
-      if (splits > 1 && ((a.out_f32 && a.batch > 1) || a.geglu)) break;
+      if (splits > 1 && ((a.out_f32 && canon_batch(a) > 1) || a.geglu)) break;
       const int per = (nk + splits - 1) / splits;
       if (per * step_k() < 512 && splits > 1) break;    // keep >= 512 of K per split
       if ((long)(splits - 1) * per >= nk) break;        // no empty split
@@ -730,7 +737,7 @@ bool eligible(const GemmArgs& a) {
   if (!vec_ok(a) && (a.rowadd || a.residual)) return false;
   if (a.rowadd && (a.rowadd_ld % 4 != 0 || ((uintptr_t)a.rowadd % 16) != 0)) return false;
   if (!is16(a.dtype) || a.K % bk != 0 || a.ldb % 8 != 0) return false;
-  if ((long)a.M * a.batch < 512) return false;     // tiny outputs: the 64x64 4-wave tiles waste less
+  if (canon_rows(a) < 512) return false;           // tiny outputs: the 64x64 4-wave tiles waste less
   if (a.geglu && (a.out_f32 || a.residual || a.batch != 1 || a.N % 128 != 0)) return false;
   if (a.conv) return !a.out_f32 && a.g.C0 % bk == 0 && a.g.C1 % bk == 0;
   return a.lda % 8 == 0 && (a.batch == 1 || a.sA % 8 == 0);
@@ -776,7 +783,7 @@ int halo_bn(const GemmArgs& a) {
   if (W < 16 || W > kHaloWMax || (W & (W - 1)) || 256 % W || g.Hin % (256 / W)) return 0;
   if ((long)g.N * g.Hin * W != a.M || a.M % 256) return 0;
   const int bn = a.N % 160 == 0 ? 160 : 0;
-  if (!bn || (g_conv_halo < 2 && (long)(a.M / 256) * (a.N / bn) < kCUs)) return 0;
+  if (!bn || (g_conv_halo < 2 && canon_rows(a) / 256 * (a.N / bn) < kCUs)) return 0;
   return bn;
 }
 

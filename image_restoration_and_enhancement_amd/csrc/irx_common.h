@@ -8,13 +8,20 @@
 
 namespace irx {
 
-enum DType : int { F32 = 0, BF16 = 1 };
+enum DType : int { F32 = 0, BF16 = 1, F16 = 2 };
 
 typedef uint16_t bf16_t;   // storage type for bfloat16
+typedef _Float16 f16_t;    // IEEE binary16 (the reference's own GPU dtype, src/inference.py:57)
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
 
 // ---------------------------------------------------------------- conversions
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
@@ -25,9 +32,11 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 template <typename T> __device__ __forceinline__ float ld_f(const T* p);
 template <> __device__ __forceinline__ float ld_f<float>(const float* p) { return *p; }
 template <> __device__ __forceinline__ float ld_f<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <> __device__ __forceinline__ float ld_f<f16_t>(const f16_t* p) { return (float)*p; }
 template <typename T> __device__ __forceinline__ T from_f(float f);
 template <> __device__ __forceinline__ float from_f<float>(float f) { return f; }
 template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float f) { return f2bf(f); }
+template <> __device__ __forceinline__ f16_t from_f<f16_t>(float f) { return (f16_t)f; }   // RNE
 
 // 16-byte vector <-> floats
 template <typename T> struct Vec16;
@@ -51,12 +60,69 @@ template <> struct Vec16<bf16_t> {
       f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
     }
   }
-  __device__ static uint4 pack(const float* f) {
+  __device__ static uint4 pack(const float* f) {   // v_cvt_pk_bf16_f32 per pair (RNE)
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i)
+      w[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){f[2 * i], f[2 * i + 1]}, bf16x2));
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
+};
+
+template <> struct Vec16<f16_t> {
+  static constexpr int N = 8;
+  __device__ static void unpack(const uint4& u, float* f) {
+    const f16x8 h = __builtin_bit_cast(f16x8, u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = (float)h[i];
+  }
+  __device__ static uint4 pack(const float* f) {   // v_cvt_pk_f16_f32 per pair (RNE)
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){f[2 * i], f[2 * i + 1]}, f16x2));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+
+// ---------------------------------------------------------------- 16-bit MFMA by storage type
+// A/B fragments are raw 16-byte (8-element) or 8-byte (4-element) register images of the storage type.
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16_t> {
+  __device__ static f32x4 m16x16x32(const uint4& a, const uint4& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  }
+  __device__ static f32x16 m32x32x16(const uint4& a, const uint4& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  }
+  __device__ static f32x4 m16x16x16(const s16x4& a, const s16x4& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+  }
+  // two fp32 -> packed pair (RNE, one v_cvt_pk_bf16_f32)
+  __device__ static uint32_t pack2(float lo, float hi) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
+  }
+  __device__ static float round(float x) { return bf2f(f2bf(x)); }   // nearest representable value
+};
+template <> struct Mfma<f16_t> {
+  __device__ static f32x4 m16x16x32(const uint4& a, const uint4& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+  }
+  __device__ static f32x16 m32x32x16(const uint4& a, const uint4& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+  }
+  __device__ static f32x4 m16x16x16(const s16x4& a, const s16x4& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(f16x4, a), __builtin_bit_cast(f16x4, b), c, 0,
+                                                 0, 0);
+  }
+  __device__ static uint32_t pack2(float lo, float hi) {   // one v_cvt_pk_f16_f32 (RNE)
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, f16x2));
+  }
+  __device__ static float round(float x) { return (float)(f16_t)x; }
 };
 
 // ---------------------------------------------------------------- activations (epilogues)
@@ -102,5 +168,6 @@ struct Error : public std::exception {
 #define IRX_LAUNCH_CHECK() IRX_HIP(hipGetLastError())
 
 inline size_t dsize(int dt) { return dt == F32 ? 4 : 2; }
+inline bool is16(int dt) { return dt == BF16 || dt == F16; }
 
 }  // namespace irx

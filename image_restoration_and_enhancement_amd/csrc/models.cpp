@@ -62,10 +62,11 @@ void Arena::free(void* p) {
 }
 
 // ---------------------------------------------------------------------------------------------- Model
-P Model::reg(const std::string& name, int layout, int dtype, std::vector<int64_t> shape) {
+P Model::reg(const std::string& name, int layout, int dtype, std::vector<int64_t> shape, float row_scale,
+            int64_t scale_rows) {
   int64_t n = 1;
   for (auto d : shape) n *= d;
-  ParamEntry e{name, layout, dtype, shape, blob_bytes_, (size_t)n * dsize(dtype)};
+  ParamEntry e{name, layout, dtype, shape, blob_bytes_, (size_t)n * dsize(dtype), row_scale, scale_rows};
   params_.push_back(e);
   P p;
   p.off = blob_bytes_;
@@ -108,6 +109,7 @@ void Model::conv2d(Ctx& c, const Act& x0, const Act* x1, P w, P b, int cout, int
   a.bias = b.set ? fptr(b) : nullptr;
   a.rowadd = rowadd; a.rowadd_ld = rowadd_ld; a.rows_per_group = out.h * out.w;
   a.residual = residual; a.ldr = a.ldc;
+  a.imgs = out.n;
   run_gemm(c, a);
 }
 
@@ -123,7 +125,7 @@ void Model::run_gemm(Ctx& c, GemmArgs& a) {
 }
 
 void Model::linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, const float* bias, void* C, long ldc,
-                   int act, const void* residual, long ldr, int out_f32) {
+                   int act, const void* residual, long ldr, int out_f32, int imgs) {
   GemmArgs a;
   a.dtype = dt_;
   a.M = M; a.N = N; a.K = K;
@@ -134,6 +136,7 @@ void Model::linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, co
   a.act = act;
   a.residual = residual; a.ldr = ldr;
   a.out_f32 = out_f32;
+  a.imgs = imgs;
   run_gemm(c, a);
 }
 
@@ -180,10 +183,15 @@ Unet::XfW Unet::make_xf(const std::string& p, int c) {
   a.nw = vec(p + "norm.weight", c); a.nb = vec(p + "norm.bias", c);
   a.piw = mat(p + "proj_in.weight", c, c); a.pib = vec(p + "proj_in.bias", c);
   a.ln1w = vec(b + "norm1.weight", c); a.ln1b = vec(b + "norm1.bias", c);
-  a.qkvw = mat(b + "attn1.to_q.weight|" + b + "attn1.to_k.weight|" + b + "attn1.to_v.weight", 3 * c, c);
+  // 16-bit engines: softmax scale * log2(e) folded into to_q (one rounding of q instead of two; the attention
+  // kernel's exp2 then needs no multiply per score)
+  const bool fold = dt_ != F32;
+  const float qs = fold ? 1.4426950408889634f / std::sqrt((float)(c / cfg_.heads)) : 1.f;
+  a.qkvw = reg(b + "attn1.to_q.weight|" + b + "attn1.to_k.weight|" + b + "attn1.to_v.weight", IRX_LAYOUT_MAT, dt_,
+               {3 * c, c}, qs, fold ? c : 0);
   a.o1w = mat(b + "attn1.to_out.0.weight", c, c); a.o1b = vec(b + "attn1.to_out.0.bias", c);
   a.ln2w = vec(b + "norm2.weight", c); a.ln2b = vec(b + "norm2.bias", c);
-  a.q2w = mat(b + "attn2.to_q.weight", c, c);
+  a.q2w = reg(b + "attn2.to_q.weight", IRX_LAYOUT_MAT, dt_, {c, c}, qs, fold ? c : 0);
   a.kv_off = kv_cols_;
   kv_cols_ += 2 * c;
   kv_names_.push_back(b + "attn2.to_k.weight");
@@ -300,17 +308,18 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   Act gn = new_act(c, B, x.h, x.w, C);
   gnorm(c, x, nullptr, a.nw, a.nb, 1e-6f, 0, gn);
   Act h = new_act(c, B, x.h, x.w, C);
-  linear(c, gn.p, C, M, C, a.piw, C, fptr(a.pib), h.p, C);
+  linear(c, gn.p, C, M, C, a.piw, C, fptr(a.pib), h.p, C, ACT_NONE, nullptr, 0, 0, B);
   drop(c, gn);
   void* n = c.ws->alloc(M * C * es);
   void* att = c.ws->alloc(M * C * es);
   // self-attention
   lnorm(c, h.p, M, C, a.ln1w, a.ln1b, 1e-5f, n);
   void* qkv = c.ws->alloc(M * 3 * C * es);
-  linear(c, n, C, M, C, a.qkvw, 3 * C, nullptr, qkv, 3 * C);
+  linear(c, n, C, M, C, a.qkvw, 3 * C, nullptr, qkv, 3 * C, ACT_NONE, nullptr, 0, 0, B);
   if (!c.ws->dry()) {
     AttnArgs aa;
     aa.dtype = dt_; aa.B = B; aa.H = heads; aa.Lq = HW; aa.Lk = HW; aa.d = d; aa.scale = scale;
+    aa.q_scaled = dt_ != F32;
     aa.q = qkv; aa.ldq = 3 * C; aa.sq = (long)HW * 3 * C;
     aa.k = (char*)qkv + C * es; aa.ldk = 3 * C; aa.sk = aa.sq;
     aa.v = (char*)qkv + 2 * C * es; aa.ldv = 3 * C; aa.sv = aa.sq;
@@ -318,20 +327,21 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     attention(aa, c.s);
   }
   c.ws->free(qkv);
-  linear(c, att, C, M, C, a.o1w, C, fptr(a.o1b), h.p, C, ACT_NONE, h.p, C);
+  linear(c, att, C, M, C, a.o1w, C, fptr(a.o1b), h.p, C, ACT_NONE, h.p, C, 0, B);
   // cross-attention (K|V precomputed per prompt)
   lnorm(c, h.p, M, C, a.ln2w, a.ln2b, 1e-5f, n);
-  linear(c, n, C, M, C, a.q2w, C, nullptr, att, C);
+  linear(c, n, C, M, C, a.q2w, C, nullptr, att, C, ACT_NONE, nullptr, 0, 0, B);
   if (!c.ws->dry()) {
     AttnArgs aa;
     aa.dtype = dt_; aa.B = B; aa.H = heads; aa.Lq = HW; aa.Lk = L; aa.d = d; aa.scale = scale;
+    aa.q_scaled = dt_ != F32;
     aa.q = att; aa.ldq = C; aa.sq = (long)HW * C;
     aa.k = (const char*)kv + a.kv_off * es; aa.ldk = kv_cols_; aa.sk = (long)L * kv_cols_;
     aa.v = (const char*)kv + (a.kv_off + C) * es; aa.ldv = kv_cols_; aa.sv = aa.sk;
     aa.o = n; aa.ldo = C; aa.so = (long)HW * C;
     attention(aa, c.s);
   }
-  linear(c, n, C, M, C, a.o2w, C, fptr(a.o2b), h.p, C, ACT_NONE, h.p, C);
+  linear(c, n, C, M, C, a.o2w, C, fptr(a.o2b), h.p, C, ACT_NONE, h.p, C, 0, B);
   // GEGLU feed-forward: fused into the projection's epilogue when the large-tile path takes the shape
   lnorm(c, h.p, M, C, a.ln3w, a.ln3b, 1e-5f, n);
   void* g = c.ws->alloc(M * 4 * C * es);
@@ -340,6 +350,7 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     ga.dtype = dt_; ga.M = M; ga.N = 8 * C; ga.K = C;
     ga.A = n; ga.lda = C; ga.B = ptr(a.ffw); ga.ldb = C;
     ga.C = g; ga.ldc = 4 * C; ga.bias = fptr(a.ffb); ga.geglu = 1;
+    ga.imgs = B;
     if (gemm_geglu_fusable(ga)) {
       run_gemm(c, ga);
     } else {
@@ -350,12 +361,12 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
       c.ws->free(ff);
     }
   }
-  linear(c, g, 4 * C, M, 4 * C, a.ff2w, C, fptr(a.ff2b), h.p, C, ACT_NONE, h.p, C);
+  linear(c, g, 4 * C, M, 4 * C, a.ff2w, C, fptr(a.ff2b), h.p, C, ACT_NONE, h.p, C, 0, B);
   c.ws->free(g);
   c.ws->free(att);
   c.ws->free(n);
   Act out = new_act(c, B, x.h, x.w, C);
-  linear(c, h.p, C, M, C, a.pow, C, fptr(a.pob), out.p, C, ACT_NONE, x.p, C);
+  linear(c, h.p, C, M, C, a.pow, C, fptr(a.pob), out.p, C, ACT_NONE, x.p, C, 0, B);
   drop(c, h);
   return out;
 }
@@ -371,9 +382,9 @@ void Unet::run(Ctx& c, const void* x, int B, int h, int w, const float* t, const
   void* te2 = c.ws->alloc((size_t)B * temb_dim_ * es);
   float* tproj = (float*)c.ws->alloc((size_t)B * temb_cols_ * sizeof(float));
   if (!c.ws->dry()) timestep_embed(dt_, t, B, bo[0], cfg_.flip_sin_to_cos, cfg_.freq_shift, te0, c.s);
-  linear(c, te0, bo[0], B, bo[0], t1w, temb_dim_, fptr(t1b), te1, temb_dim_, ACT_SILU);
-  linear(c, te1, temb_dim_, B, temb_dim_, t2w, temb_dim_, fptr(t2b), te2, temb_dim_, ACT_SILU);
-  linear(c, te2, temb_dim_, B, temb_dim_, tpw, temb_cols_, fptr(tpb), tproj, temb_cols_, ACT_NONE, nullptr, 0, 1);
+  linear(c, te0, bo[0], B, bo[0], t1w, temb_dim_, fptr(t1b), te1, temb_dim_, ACT_SILU, nullptr, 0, 0, B);
+  linear(c, te1, temb_dim_, B, temb_dim_, t2w, temb_dim_, fptr(t2b), te2, temb_dim_, ACT_SILU, nullptr, 0, 0, B);
+  linear(c, te2, temb_dim_, B, temb_dim_, tpw, temb_cols_, fptr(tpb), tproj, temb_cols_, ACT_NONE, nullptr, 0, 1, B);
   c.ws->free(te0);
   c.ws->free(te1);
   c.ws->free(te2);
@@ -468,7 +479,8 @@ void Unet::prepare_context(hipStream_t s, const void* ctx, int B, int L, void* k
   Arena ar;
   ar.reset(ws ? ws : (char*)16, cap);   // no temporaries needed
   Ctx c{s, &ar};
-  linear(c, ctx, cfg_.cross_attention_dim, B * L, cfg_.cross_attention_dim, kvw, kv_cols_, nullptr, kv, kv_cols_);
+  linear(c, ctx, cfg_.cross_attention_dim, B * L, cfg_.cross_attention_dim, kvw, kv_cols_, nullptr, kv, kv_cols_,
+         ACT_NONE, nullptr, 0, 0, B);
 }
 
 // ---------------------------------------------------------------------------------------------- VAE
@@ -582,7 +594,7 @@ Act Vae::attn(Ctx& c, const AttW& a, Act& x) {
   Act gn = new_act(c, B, x.h, x.w, C);
   gnorm(c, x, nullptr, a.gw, a.gb, cfg_.norm_eps, 0, gn);
   void* qkv = c.ws->alloc(M * 3 * C * es);
-  linear(c, gn.p, C, M, C, a.qkvw, 3 * C, fptr(a.qkvb), qkv, 3 * C);
+  linear(c, gn.p, C, M, C, a.qkvw, 3 * C, fptr(a.qkvb), qkv, 3 * C, ACT_NONE, nullptr, 0, 0, B);
   drop(c, gn);
   float* S = (float*)c.ws->alloc((size_t)B * HW * HWp * sizeof(float));
   if (!c.ws->dry()) {
@@ -593,6 +605,7 @@ Act Vae::attn(Ctx& c, const AttW& a, Act& x) {
     g.C = S; g.ldc = HWp; g.sC = (long)HW * HWp; g.out_f32 = 1;
     g.alpha = 1.0f / std::sqrt((float)C);
     g.batch = B;
+    g.imgs = B;
     gemm(g, c.s);
   }
   void* P = c.ws->alloc((size_t)B * HW * HWp * es);
@@ -612,12 +625,13 @@ Act Vae::attn(Ctx& c, const AttW& a, Act& x) {
     g.B = VT; g.ldb = HWp; g.sB = (long)C * HWp;
     g.C = O; g.ldc = C; g.sC = (long)HW * C;
     g.batch = B;
+    g.imgs = B;
     gemm(g, c.s);
   }
   c.ws->free(P);
   c.ws->free(VT);
   Act out = new_act(c, B, x.h, x.w, C);
-  linear(c, O, C, M, C, a.ow, C, fptr(a.ob), out.p, C, ACT_NONE, x.p, C);
+  linear(c, O, C, M, C, a.ow, C, fptr(a.ob), out.p, C, ACT_NONE, x.p, C, 0, B);
   c.ws->free(O);
   return out;
 }
@@ -656,7 +670,7 @@ void Vae::run_encode(Ctx& c, const void* img, int B, int H, int W, void* moments
   Act co = new_act(c, B, gn.h, gn.w, 8);
   conv2d(c, gn, nullptr, e_cout_w, e_cout_b, 8, 3, 1, 1, 1, gn.h, gn.w, co);
   drop(c, gn);
-  linear(c, co.p, 8, co.pix(), 8, qw, 8, fptr(qb), moments, 8);
+  linear(c, co.p, 8, co.pix(), 8, qw, 8, fptr(qb), moments, 8, ACT_NONE, nullptr, 0, 0, B);
   drop(c, co);
 }
 
@@ -665,7 +679,7 @@ void Vae::run_decode(Ctx& c, const void* z, int B, int h, int w, void* out) {
   const int nb = cfg_.n_blocks;
   const int cm = bo[nb - 1];
   Act zq = new_act(c, B, h, w, 8);
-  linear(c, z, 8, (long)B * h * w, 8, pqw, 8, fptr(pqb), zq.p, 8);
+  linear(c, z, 8, (long)B * h * w, 8, pqw, 8, fptr(pqb), zq.p, 8, ACT_NONE, nullptr, 0, 0, B);
   Act cur = new_act(c, B, h, w, cm);
   conv2d(c, zq, nullptr, d_cin_w, d_cin_b, cm, 3, 1, 1, 1, h, w, cur);
   drop(c, zq);

@@ -35,6 +35,8 @@ struct ParamEntry {
   int layout, dtype;
   std::vector<int64_t> shape;
   size_t off, bytes;
+  float row_scale = 1.f;     // packer scales rows [0, scale_rows) (folded attention scale)
+  int64_t scale_rows = 0;
 };
 
 struct Act {   // NHWC activation view
@@ -54,7 +56,8 @@ class Model {
   void bind(void* blob, size_t bytes);
 
  protected:
-  P reg(const std::string& name, int layout, int dtype, std::vector<int64_t> shape);
+  P reg(const std::string& name, int layout, int dtype, std::vector<int64_t> shape, float row_scale = 1.f,
+        int64_t scale_rows = 0);
   P vec(const std::string& name, int64_t n) { return reg(name, IRX_LAYOUT_VEC, F32, {n}); }
   P mat(const std::string& name, int64_t n, int64_t k) { return reg(name, IRX_LAYOUT_MAT, dt_, {n, k}); }
   P conv(const std::string& name, int64_t co, int64_t kh, int64_t kw, int64_t ci) {
@@ -71,7 +74,7 @@ class Model {
               int hv, int wv, const Act& out, const float* rowadd = nullptr, long rowadd_ld = 0,
               const void* residual = nullptr, int out_f32 = 0, int ldc = -1);
   void linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, const float* bias, void* C, long ldc,
-              int act = ACT_NONE, const void* residual = nullptr, long ldr = 0, int out_f32 = 0);
+              int act = ACT_NONE, const void* residual = nullptr, long ldr = 0, int out_f32 = 0, int imgs = 0);
   void run_gemm(Ctx& c, GemmArgs& a);   // allocates split-K partials from the workspace when needed
   void gnorm(Ctx& c, const Act& x0, const Act* x1, P g, P b, float eps, int silu, const Act& out);
   void lnorm(Ctx& c, const void* x, int rows, int C, P g, P b, float eps, void* out);

@@ -29,8 +29,10 @@ int gn_slabs(int C, int vec, int G) {
     if (nv % s == 0 && (C / s) % (C / G) == 0 && nv / s <= 256) return s;
   return 0;
 }
-// pixel chunks per (image, slab): ~2048 blocks in all, >= 4 pixels per thread, <= kMaxChunks
-int gn_chunks3(int N, int HW, int slabs, int rows) {
+// pixel chunks per (image, slab): ~2048 blocks at kCanonImages images, >= 4 pixels per thread, <= kMaxChunks.
+// A function of the per-image shape only, so an image's statistics (and bits) do not depend on the batch.
+int gn_chunks3(int HW, int slabs, int rows) {
+  const int N = kCanonImages;
   const int want = (2048 + N * slabs - 1) / (N * slabs);
   const int most = std::max(1, HW / (4 * rows));
   return std::max(1, std::min(std::min(want, most), kMaxChunks));
@@ -329,7 +331,7 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
   if (g_gn_v2 && N <= 4096 && slabs > 0) {
     ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_stats3_kernel") : std::string(), 0.0, s);
     const int rows3 = 256 / (C / slabs / VEC);
-    const int nch3 = gn_chunks3(N, HW, slabs, rows3);
+    const int nch3 = gn_chunks3(HW, slabs, rows3);
     gn_stats3_kernel<T><<<dim3(nch3, N, slabs), 256, 0, s>>>(
         (const T*)x0, (const T*)x1, C0, C1, HW, G, (HW + nch3 - 1) / nch3, part);
     IRX_LAUNCH_CHECK();
@@ -387,6 +389,7 @@ void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N
   IRX_CHECK(C <= 8192, "GroupNorm: too many channels");
   IRX_CHECK(C1 == 0 || x1, "GroupNorm: concat source missing");
   if (dtype == F32) gn_t<float>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s);
+  else if (dtype == F16) gn_t<f16_t>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s);
   else gn_t<bf16_t>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s);
 }
 
@@ -395,6 +398,7 @@ void layer_norm(int dtype, const void* x, long ldx, int rows, int C, float eps, 
   const int vec = dtype == F32 ? 4 : 8;
   IRX_CHECK(C % vec == 0 && ldx % vec == 0 && ldo % vec == 0, "LayerNorm: rows must be 16-byte multiples");
   if (dtype == F32) ln_t<float>(x, ldx, rows, C, eps, gamma, beta, out, ldo, s);
+  else if (dtype == F16) ln_t<f16_t>(x, ldx, rows, C, eps, gamma, beta, out, ldo, s);
   else ln_t<bf16_t>(x, ldx, rows, C, eps, gamma, beta, out, ldo, s);
 }
 

@@ -35,6 +35,9 @@ struct GemmArgs {
   float out_scale = 1.f;
   int act = ACT_NONE;     // applied after bias/rowadd, before residual
   int batch = 1;
+  // images spanned by the M x batch rows (0: not image-indexed).  Tile / split-K / kernel choices are made for
+  // the canonical kCanonImages images, so an image's bits never depend on how many images share its batch.
+  int imgs = 0;
   int vec_epilogue = 0;   // set by the launcher: 16-byte LDS-staged output path is legal for this call
   // GEGLU epilogue: B rows interleaved in (64 value, 64 gate) blocks (IRX_LAYOUT_*_GEGLU64); C gets N/2
   // columns h * gelu(g).  Only the large-tile path fuses it (gemm_geglu_fusable); else see geglu().
@@ -42,6 +45,7 @@ struct GemmArgs {
   void* splitk_ws = nullptr; size_t splitk_ws_bytes = 0;   // caller workspace for split-K partials
   int dbg = 0;            // large-tile diagnostics (irx_set_option("gemm_dbg")): 1 skip epilogue, 2 skip MFMAs
 };
+constexpr int kCanonImages = 16;
 void gemm(const GemmArgs& a, hipStream_t s);
 bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path; false if not eligible
 size_t gemm_workspace_bytes(const GemmArgs& a);           // split-K partial buffer the call will use
@@ -78,9 +82,16 @@ struct AttnArgs {
   void* o = nullptr; long ldo = 0, so = 0;
   float scale = 1.f;
   int causal = 0;
+  // head strides in elements (0: heads interleaved in a row, stride d) — a head-major [b][h][L][d] tensor
+  // passes hs* = L * d and ld* = d
+  long hsq = 0, hsk = 0, hsv = 0, hso = 0;
+  int q_scaled = 0;       // q already multiplied by scale * log2(e) (folded into the to_q weights)
+  int xcd = 0;            // (set by the launcher) XCD-grouped block order
 };
 void attention(const AttnArgs& a, hipStream_t s);
 extern bool g_attn_v2;
+extern int g_attn_v3;    // 32x32x16 kernel for bf16 / fp16 (0: the round-1 kernels, bf16 only)
+extern int g_attn_xcd;   // 1: (batch, head) groups of q-blocks kept on one XCD (K/V shared in its L2)
 extern int g_attn_d40;   // bf16: 16x16x32 kernel (irx_set_option("attn_v2", 0) selects the 16x16x16 one)
 
 // ------------------------------------------------------------ elementwise / data movement

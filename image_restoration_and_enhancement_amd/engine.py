@@ -18,15 +18,16 @@ import torch.nn.functional as F
 from . import _lib as L
 from .configs import UNetConfig, VAEConfig, CLIPConfig
 
-DTYPES = {"fp32": L.IRX_F32, "float32": L.IRX_F32, "bf16": L.IRX_BF16, "bfloat16": L.IRX_BF16}
-TORCH_DT = {L.IRX_F32: torch.float32, L.IRX_BF16: torch.bfloat16}
+DTYPES = {"fp32": L.IRX_F32, "float32": L.IRX_F32, "bf16": L.IRX_BF16, "bfloat16": L.IRX_BF16,
+          "fp16": L.IRX_F16, "float16": L.IRX_F16, "half": L.IRX_F16}
+TORCH_DT = {L.IRX_F32: torch.float32, L.IRX_BF16: torch.bfloat16, L.IRX_F16: torch.float16}
 
 
 def dtype_code(dtype) -> int:
     if isinstance(dtype, int):
         return dtype
     if isinstance(dtype, torch.dtype):
-        return L.IRX_F32 if dtype == torch.float32 else L.IRX_BF16
+        return {torch.float32: L.IRX_F32, torch.bfloat16: L.IRX_BF16, torch.float16: L.IRX_F16}[dtype]
     return DTYPES[str(dtype)]
 
 
@@ -77,6 +78,8 @@ class ParamSpec:
     shape: Tuple[int, ...]
     offset: int
     nbytes: int
+    row_scale: float = 1.0
+    scale_rows: int = 0
 
 
 def geglu64_order(n: int) -> torch.Tensor:
@@ -143,7 +146,7 @@ class NativeModel:
             L.call("irx_model_param_info", self.h, i, C.byref(info))
             out.append(ParamSpec(info.name.decode(), info.layout, info.dtype,
                                  tuple(int(info.shape[k]) for k in range(info.ndim)), int(info.offset),
-                                 int(info.bytes)))
+                                 int(info.bytes), float(info.row_scale), int(info.scale_rows)))
         return out
 
     def blob_bytes(self) -> int:
@@ -157,6 +160,9 @@ class NativeModel:
         for p in self.manifest():
             parts = [_convert(sd[n], p.layout) for n in p.name.split("|")]
             t = parts[0] if len(parts) == 1 else torch.cat(parts, dim=0)
+            if p.scale_rows:
+                t = t.clone()
+                t[:p.scale_rows] *= p.row_scale
             t = _pad_to(t, p.shape).to(TORCH_DT[p.dtype]).contiguous()
             if t.numel() * t.element_size() != p.nbytes:
                 raise ValueError(f"{p.name}: packed {t.numel() * t.element_size()} bytes, manifest {p.nbytes}")

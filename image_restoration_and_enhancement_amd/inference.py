@@ -17,8 +17,9 @@ Differences that follow from the engine (documented in INTEGRATION.md):
 * the diffusion path needs a ROCm GPU; on a CPU-only host the loaders fail and the classical fallbacks
   run (the reference would run diffusers on the CPU).  A missing or unloadable `libirx.so` is never
   hidden: `IrxError` propagates out of every entry point (no silent fallback).
-* compute dtype is bf16 on the GPU (the reference uses fp16); `config["engine"] = {"dtype": "fp32"}`
-  selects the fp32 engine that matches the reference CPU path within 1e-3 per pixel.
+* compute dtype is bf16 on the GPU by default; `config["engine"] = {"dtype": "fp16"}` selects the
+  reference's own GPU dtype (src/inference.py:57) and `{"dtype": "fp32"}` the fp32 engine that matches the
+  reference CPU path within 1e-3 per pixel.
 * noise is drawn from `torch.Generator("cpu").manual_seed(seed)` — the reference's CPU-path draws.
 * weights load from the task's saved `best/` directory (safetensors) or, in pretrained mode
   (`fine_tuned_dir == "nonexistent"`), from a local Hugging Face cache snapshot of `pretrained_id` (no
@@ -93,10 +94,11 @@ class RestorationPipeline:
             self.device = device
         engine_cfg = dict((config or {}).get("engine", {}))
         self.engine_dtype = engine_cfg.get("dtype", "bf16")
-        if self.engine_dtype not in ("bf16", "fp32"):
-            raise ValueError(f"engine dtype must be 'bf16' or 'fp32', got {self.engine_dtype!r}")
+        if self.engine_dtype not in ("bf16", "fp16", "fp32"):
+            raise ValueError(f"engine dtype must be 'bf16', 'fp16' or 'fp32', got {self.engine_dtype!r}")
         on_gpu = self.device.startswith("cuda")
-        self.dtype = (torch.bfloat16 if self.engine_dtype == "bf16" else torch.float32) if on_gpu else torch.float32
+        self.dtype = ({"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[self.engine_dtype]
+                      if on_gpu else torch.float32)
         self.models: dict[str, object] = {}
         self.seed = seed
         logger.info(f"Using device: {self.device} ({self.dtype}), seed: {seed}")
@@ -446,7 +448,8 @@ class RestorationPipeline:
                   "colorize": self.load_colorize_model, "inpaint": self.load_inpaint_model}[task]
         loader()
         model = self.models.get(task)
-        single = {"denoise": lambda im, mk: self.denoise(im, **({"strength": strength} if strength else {})),
+        single = {"denoise": lambda im, mk: self.denoise(im, **({"strength": strength} if strength is not None
+                                                                else {})),
                   "sr": lambda im, mk: self.super_resolve(im),
                   "colorize": lambda im, mk: self.colorize(im),
                   "inpaint": lambda im, mk: self.inpaint(im, mask=mk)}[task]
@@ -478,10 +481,16 @@ class RestorationPipeline:
             for k in range(0, len(idx), max_batch):
                 chunk = idx[k:k + max_batch]
                 ims = [prepared[i][0] for i in chunk]
-                if task == "inpaint":
-                    res = self._inpaint_native(model, ims, [prepared[i][1] for i in chunk], p, s, steps, g)
-                else:
-                    res = self._img2img(model, ims, p, s, steps, g)
+                try:
+                    if task == "inpaint":
+                        res = self._inpaint_native(model, ims, [prepared[i][1] for i in chunk], p, s, steps, g)
+                    else:
+                        res = self._img2img(model, ims, p, s, steps, g)
+                except IrxError:
+                    raise
+                except Exception as e:     # as the single-image entry points: log, then their fallbacks
+                    logger.warning(f"batched {task} failed ({e}); running the single-image entry point per image")
+                    res = [single(images[i], masks[i]) for i in chunk]
                 for i, r in zip(chunk, res):
                     out[i] = r
         return out  # type: ignore[return-value]

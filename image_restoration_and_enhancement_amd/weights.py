@@ -230,16 +230,38 @@ def random_state_dict(kind: str, cfg, seed: int = 0) -> Dict[str, torch.Tensor]:
 _LEGACY_VAE_ATTN = {"query.": "to_q.", "key.": "to_k.", "value.": "to_v.", "proj_attn.": "to_out.0."}
 
 
-def load_component_dir(path: str | Path) -> Dict[str, torch.Tensor]:
-    """Read every *.safetensors file of one saved component directory (no pickle loading)."""
-    from safetensors.torch import load_file
+_WEIGHT_NAMES = ("diffusion_pytorch_model", "model")
+
+
+def component_weight_files(path: str | Path, variant: str | None = None) -> list:
+    """The safetensors file(s) diffusers / transformers `from_pretrained(..., use_safetensors=True,
+    variant=variant)` would read from one component directory: `<name>[.<variant>].safetensors`, or the
+    shards its `<name>[.<variant>].safetensors.index.json` lists.  Other files (`.fp16` / `.non_ema` variants
+    next to the plain file) are ignored unless that variant is asked for."""
+    import json
 
     p = Path(path)
-    files = sorted(p.glob("*.safetensors"))
-    if not files:
-        raise FileNotFoundError(f"no .safetensors weights under {p}")
+    suffix = f".{variant}.safetensors" if variant else ".safetensors"
+    for name in _WEIGHT_NAMES:
+        f = p / (name + suffix)
+        if f.exists():
+            return [f]
+        idx = p / (name + suffix + ".index.json")
+        if idx.exists():
+            shards = sorted(set(json.loads(idx.read_text())["weight_map"].values()))
+            return [p / s for s in shards]
+    found = sorted(x.name for x in p.glob("*.safetensors"))
+    raise FileNotFoundError(f"no {'|'.join(_WEIGHT_NAMES)}{suffix} (or its .index.json) under {p}"
+                            + (f"; found {found}" if found else ""))
+
+
+def load_component_dir(path: str | Path, variant: str | None = None) -> Dict[str, torch.Tensor]:
+    """Read one saved component directory's weights (safetensors only: no pickle loading), chosen as
+    diffusers chooses them (component_weight_files)."""
+    from safetensors.torch import load_file
+
     sd: Dict[str, torch.Tensor] = {}
-    for f in files:
+    for f in component_weight_files(path, variant):
         sd.update(load_file(str(f)))
     out = {}
     for k, v in sd.items():

@@ -9,7 +9,7 @@
  *     src/inference.py:496-498, :575-577, :679-681, :774-776);
  *   - tensors are raw DEVICE pointers owned by the caller (PyTorch-ROCm tensors used as
  *     containers); the library never allocates or frees caller memory;
- *   - activations are NHWC; `dtype` is IRX_F32 (parity mode) or IRX_BF16 (throughput mode);
+ *   - activations are NHWC; `dtype` is IRX_F32 (parity mode), IRX_BF16 or IRX_F16 (throughput modes);
  *   - `stream` is a hipStream_t passed as void*; work is enqueued, nothing synchronises;
  *   - a model handle is not thread-safe; use one handle per stream.
  */
@@ -24,6 +24,7 @@ extern "C" {
 
 #define IRX_F32 0
 #define IRX_BF16 1
+#define IRX_F16 2   /* IEEE half: the reference's own GPU dtype (src/inference.py:57), BASELINE configs[4] */
 
 #define IRX_MODEL_UNET 0
 #define IRX_MODEL_VAE 1
@@ -68,6 +69,10 @@ typedef struct {
   int64_t shape[4];   /* engine shape (padded) */
   size_t offset;      /* byte offset in the weight blob */
   size_t bytes;
+  /* the packer multiplies rows [0, scale_rows) by row_scale (in fp32, before the cast): the attention
+   * softmax scale * log2(e) folded into to_q in the 16-bit engines (the kernels then take q pre-scaled) */
+  float row_scale;
+  int64_t scale_rows;
 } irx_param_info;
 
 const char* irx_last_error(void);
@@ -209,6 +214,9 @@ int irx_op_layer_norm(void* stream, int dtype, const void* x, int rows, int c, f
 int irx_op_attention(void* stream, int dtype, int batch, int heads, int lq, int lk, int d, const void* q, long ldq,
                      long sq, const void* k, long ldk, long sk, const void* v, long ldv, long sv, void* o, long ldo,
                      long so, float scale, int causal);
+/* heads laid out [batch][heads][len][d] (q, k, v and o), contiguous */
+int irx_op_attention_hm(void* stream, int dtype, int batch, int heads, int lq, int lk, int d, const void* q,
+                        const void* k, const void* v, void* o, float scale);
 int irx_op_geglu(void* stream, int dtype, const void* proj, int M, int F, void* out);
 /* C[M][N/2] = GEGLU(A B^T + bias) with B/bias in the GEGLU64 row order (fused epilogue, bf16 large tiles) */
 int irx_op_gemm_geglu(void* stream, int dtype, int M, int N, int K, const void* A, const void* B, const float* bias,

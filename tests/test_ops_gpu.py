@@ -1,8 +1,8 @@
 """GPU parity of every hand-written kernel (through the C ABI) against fp32 PyTorch-CPU references.
 
 Tolerances (max |err| / max |ref|): fp32 path 1e-4 (exact-f32 MFMA / fp32 VALU, different
-summation order only); bf16 path 2e-2 (bf16 storage of inputs/outputs, fp32 accumulation) with
-the reference fed the same bf16-rounded inputs.
+summation order only); bf16 path 2e-2, fp16 path 5e-3 (16-bit storage of inputs/outputs, fp32
+accumulation) with the reference fed the same rounded inputs.
 """
 import math
 
@@ -14,8 +14,9 @@ from tests import opref as O
 
 pytestmark = pytest.mark.gpu
 
-TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2}
-DTS = [torch.float32, torch.bfloat16]
+TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2, torch.float16: 5e-3}
+DTS = [torch.float32, torch.bfloat16, torch.float16]
+DT16 = [torch.bfloat16, torch.float16]
 
 
 def _r(*shape, seed=0, scale=1.0):
@@ -180,7 +181,7 @@ def test_attention(device, dt, B, Lq, Lk, C, heads, causal):
     q, k, v = _r(B, Lq, C, seed=50), _r(B, Lk, C, seed=51), _r(B, Lk, C, seed=52)
     got = O.attention(_dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device), heads, causal)
     ref = O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), heads, causal)
-    assert O.rel_err(got, ref) < TOL[dt] * (2 if dt == torch.bfloat16 else 1)
+    assert O.rel_err(got, ref) < TOL[dt] * (1 if dt == torch.float32 else 2)
 
 
 @pytest.mark.parametrize("dt", DTS)
@@ -191,7 +192,7 @@ def test_attention_fused_qkv_strides(device, dt):
     got = O.attention(qkv[:, :, :C], qkv[:, :, C:2 * C], qkv[:, :, 2 * C:], heads)
     c = qkv.float().cpu()
     ref = O.ref_attention(c[:, :, :C], c[:, :, C:2 * C], c[:, :, 2 * C:], heads)
-    assert O.rel_err(got, ref) < TOL[dt] * (2 if dt == torch.bfloat16 else 1)
+    assert O.rel_err(got, ref) < TOL[dt] * (1 if dt == torch.float32 else 2)
 
 
 @pytest.mark.parametrize("dt", DTS)
@@ -202,7 +203,7 @@ def test_attention_softmax_spike(device, dt):
     k[:, 200] = q[:, 3] * 4.0
     got = O.attention(_dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device), heads)
     ref = O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), heads)
-    assert O.rel_err(got, ref) < TOL[dt] * (2 if dt == torch.bfloat16 else 1)
+    assert O.rel_err(got, ref) < TOL[dt] * (1 if dt == torch.float32 else 2)
 
 
 @pytest.mark.parametrize("dt", DTS)
@@ -238,8 +239,8 @@ def tiles(request):
     (2, 48, 48, 96, 32, 128, 3, 1, 1, None),        # channels % 32 only   -> ring path only (BK 32)
     (1, 16, 16, 1280, 1280, 1280, 3, 1, 1, None),   # long K, few tiles    -> split-K
 ])
-def test_conv_large(device, tiles, case):
-    dt = torch.bfloat16
+@pytest.mark.parametrize("dt", DT16)
+def test_conv_large(device, tiles, case, dt):
     N, H, W, C0, C1, Co, k, s, p, up = case
     x0 = _r(N, C0, H, W, seed=70)
     x1 = _r(N, C1, H, W, seed=71) if C1 else None
@@ -258,8 +259,8 @@ def test_conv_large(device, tiles, case):
 @pytest.mark.parametrize("M,N,K,res,f32", [(8192, 2560, 320, False, False), (4096, 320, 1280, True, False),
                                            (5000, 640, 640, True, True), (4096, 512, 512, False, False),
                                            (6144, 384, 128, False, True)])
-def test_gemm_large(device, tiles, M, N, K, res, f32):
-    dt = torch.bfloat16
+@pytest.mark.parametrize("dt", DT16)
+def test_gemm_large(device, tiles, M, N, K, res, f32, dt):
     A = _r(M, K, seed=74)
     Bw = _r(N, K, seed=75, scale=1 / math.sqrt(K))
     bias = _r(N, seed=76)
@@ -270,19 +271,19 @@ def test_gemm_large(device, tiles, M, N, K, res, f32):
     assert O.rel_err(got, ref) < TOL[dt]
 
 
+@pytest.mark.parametrize("dt", DT16)
 @pytest.mark.parametrize("M,C", [(8192, 320), (4096, 640)])
-def test_gemm_geglu_fused(device, M, C):
+def test_gemm_geglu_fused(device, M, C, dt):
     """ff.net.0.proj + GEGLU in one kernel (GEGLU64 weight order) vs Linear -> chunk -> h * gelu(g)."""
     from image_restoration_and_enhancement_amd import _lib as L
     from image_restoration_and_enhancement_amd.engine import geglu64_order
-    dt = torch.bfloat16
     A = _r(M, C, seed=80)
     Wt = _r(8 * C, C, seed=81, scale=1 / math.sqrt(C))
     bias = _r(8 * C, seed=82)
     perm = geglu64_order(8 * C)
     out = torch.empty(M, 4 * C, dtype=dt, device=device)
     a_d, w_d, b_d = _dev(A, dt, device), _dev(Wt[perm], dt, device), bias[perm].to(device).contiguous()
-    L.call("irx_op_gemm_geglu", O.S(), L.IRX_BF16, M, 8 * C, C, O.P(a_d), O.P(w_d), O.P(b_d), O.P(out))
+    L.call("irx_op_gemm_geglu", O.S(), O.DT[dt], M, 8 * C, C, O.P(a_d), O.P(w_d), O.P(b_d), O.P(out))
     pr = _q(A, dt) @ _q(Wt, dt).T + bias
     h, g = pr.chunk(2, dim=-1)
     assert O.rel_err(out, h * F.gelu(g)) < TOL[dt]
@@ -336,8 +337,8 @@ def halo_forced():
     (1, 8, 16, 64, 0, 160, False),      # W 16 needs 16-row images: falls back to the im2col walk
     (1, 16, 16, 64, 64, 160, False),    # W 16: one tile per image
 ])
-def test_conv_halo(device, halo_forced, case):
-    dt = torch.bfloat16
+@pytest.mark.parametrize("dt", DT16)
+def test_conv_halo(device, halo_forced, case, dt):
     N, H, W, C0, C1, Co, extra = case
     x0 = _r(N, C0, H, W, seed=80)
     x1 = _r(N, C1, H, W, seed=81) if C1 else None
@@ -368,10 +369,12 @@ def test_attention_d40_variants(device, variant, B, Lq, Lk):
     dt = torch.bfloat16
     q, k, v = _r(B, Lq, 320, seed=60), _r(B, Lk, 320, seed=61), _r(B, Lk, 320, seed=62)
     L.call("irx_set_option", b"attn_d40", variant)
+    L.call("irx_set_option", b"attn_v3", 0)          # the round-1 kernels (attn3 is the default)
     try:
         got = O.attention(_dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device), 8)
     finally:
         L.call("irx_set_option", b"attn_d40", 2)
+        L.call("irx_set_option", b"attn_v3", 1)
     ref = O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), 8)
     assert O.rel_err(got, ref) < 2 * TOL[dt]
 
@@ -397,3 +400,22 @@ def test_gemm_splitk_two_streams(device):
     for i in range(2):
         for o in outs[i]:
             assert torch.equal(o, want[i])
+
+
+@pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("B,Lq,Lk,C,heads", [(2, 256, 256, 320, 8), (1, 333, 190, 640, 8), (2, 130, 77, 1280, 8)])
+def test_attention_v3_vs_v2_and_head_major(device, dt, B, Lq, Lk, C, heads):
+    """attn3 with heads laid out [b][h][L][d] (head strides) equals the interleaved layout bit for bit, and
+    (bf16) agrees with the round-1 kernel within the bf16 bound."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    d = C // heads
+    q, k, v = _r(B, Lq, C, seed=63), _r(B, Lk, C, seed=64), _r(B, Lk, C, seed=65)
+    qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
+    got = O.attention(qd, kd, vd, heads)
+    hm = [x.view(B, x.shape[1], heads, d).transpose(1, 2).contiguous() for x in (qd, kd, vd)]
+    o = torch.empty(B, heads, Lq, d, dtype=dt, device=device)
+    L.call("irx_op_attention_hm", O.S(), O.DT[dt], B, heads, Lq, Lk, d, O.P(hm[0]), O.P(hm[1]), O.P(hm[2]),
+           O.P(o), 1.0 / math.sqrt(d))
+    assert torch.equal(o.transpose(1, 2).reshape(B, Lq, C), got)
+    ref = O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), heads)
+    assert O.rel_err(got, ref) < 2 * TOL[dt]

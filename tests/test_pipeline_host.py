@@ -45,7 +45,9 @@ def test_constructor_attributes():
                                                                    "pretrained_id": "x/y"}})
     assert p2.config["denoise"]["fine_tuned_dir"] == "nonexistent" and "sr" in p2.config
     with pytest.raises(ValueError):
-        INF.RestorationPipeline(device="cpu", config={"engine": {"dtype": "fp16"}})
+        INF.RestorationPipeline(device="cpu", config={"engine": {"dtype": "int8"}})
+    p3 = INF.RestorationPipeline(device="cpu", config={"engine": {"dtype": "fp16"}})
+    assert p3.engine_dtype == "fp16" and p3.dtype == torch.float32      # CPU host: fallbacks only
 
 
 def test_fallbacks_without_gpu(tmp_path, monkeypatch):
@@ -190,3 +192,22 @@ def test_prediction_driver_layout(tmp_path):
     assert Image.open(out / "denoise" / "test" / "a.png").size == (16, 16)
     assert Image.open(out / "sr_x4" / "test" / "a.png").size == (64, 64)
     assert (out / "colorize" / "test" / "a.png").exists() and (out / "inpaint" / "test" / "a.png").exists()
+
+
+def test_restore_batch_strength_zero_and_fallback(tmp_path, monkeypatch):
+    """restore_batch keeps strength=0.0 (not 'unset'), and a failing batched engine call falls back per image
+    to the single-image entry point, as _denoise_sd does."""
+    monkeypatch.chdir(tmp_path)
+    p = INF.RestorationPipeline(device="cpu")
+    img = rgb(12, 16, seed=3)
+    got = p.restore_batch("denoise", [img], strength=0.0)[0]
+    assert np.array_equal(np.array(got), np.array(p.denoise(img, strength=0.0)))
+
+    def engine_fails(*a, **k):
+        raise ValueError("strength too small: no denoising steps")
+
+    monkeypatch.setattr(p, "load_denoise_model", lambda: None)
+    p.models["denoise"] = INF.NativeSDModel(None, "img2img", "test")
+    monkeypatch.setattr(p, "_img2img", engine_fails)
+    out = p.restore_batch("denoise", [img, rgb(12, 16, seed=4)], strength=0.0)
+    assert np.array_equal(np.array(out[0]), np.array(CL.denoise_opencv(img, 0.0)))
