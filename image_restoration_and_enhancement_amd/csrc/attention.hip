@@ -553,8 +553,9 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
   constexpr int NCH = (KT * CPR + 255) / 256;
   constexpr float THR = 8.f;
   static_assert(D % 8 == 0 && KT % 32 == 0, "attn3 shape");
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[KT * SK];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[KT * SV];
+  // two LDS stages: tile j+1 is written under tile j's compute, one barrier per tile
+  __shared__ __attribute__((aligned(16))) uint16_t Ks2[2 * KT * SK];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs2[2 * KT * SV];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5, g = lane >> 4;
@@ -569,8 +570,9 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
   const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : D);
   const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : D);
 
-  for (int i = tid; i < KT * SK; i += 256) Ks[i] = 0;
-  for (int i = tid; i < KT * SV; i += 256) Vs[i] = (ONES && i % SV == D) ? one_bits<T>() : (uint16_t)0;
+  // pad columns: K[.][d] = 1 when -m rides in the padding (PADM below), V[.][d] = 1 for the row sums
+  for (int i = tid; i < 2 * KT * SK; i += 256) Ks2[i] = (DQ > D && i % SK == D) ? one_bits<T>() : (uint16_t)0;
+  for (int i = tid; i < 2 * KT * SV; i += 256) Vs2[i] = (ONES && i % SV == D) ? one_bits<T>() : (uint16_t)0;
 
   // Q^T fragments (B operand): lane (r, hh) holds q[qrow][16s + 8hh .. +7], pre-scaled by scale*log2(e)
   uint4 qf[NS];
@@ -609,41 +611,60 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
       if (hh) qf[PADS].x = (qf[PADS].x & 0xFFFF0000u) | (Mfma<T>::pack2(-m, 0.f) & 0xFFFFu);
     }
   };
-  if constexpr (PADM)
-    for (int i = tid; i < KT; i += 256) Ks[i * SK + D] = one_bits<T>();
 
   const int kend = CAUSAL ? min(a.Lk, qb * QB + QB) : a.Lk;
+  // per-thread staging slots (row, 16-byte chunk) of a K/V tile, fixed for the kernel: pointers and LDS offsets
+  // computed once; a full tile (every row < Lk) loads with no per-row checks
   uint4 kreg[NCH], vreg[NCH];
-  auto load = [&](int j0) {
+  const T* kp[NCH];
+  const T* vp[NCH];
+  int krow[NCH], ksoff[NCH], vsoff[NCH];
 #pragma unroll
-    for (int u = 0; u < NCH; ++u) {
-      const int idx = tid + 256 * u;
-      kreg[u] = make_uint4(0, 0, 0, 0);
-      vreg[u] = make_uint4(0, 0, 0, 0);
-      if (idx < KT * CPR) {
-        const int row = idx / CPR, c = idx - row * CPR;
-        if (j0 + row < a.Lk) {
-          kreg[u] = *(const uint4*)(K + (long)(j0 + row) * a.ldk + c * 8);
-          vreg[u] = *(const uint4*)(V + (long)(j0 + row) * a.ldv + c * 8);
+  for (int u = 0; u < NCH; ++u) {
+    const int idx = min(tid + 256 * u, KT * CPR - 1);
+    const int row = idx / CPR, c = idx - row * CPR;
+    krow[u] = row;
+    kp[u] = K + (long)row * a.ldk + c * 8;
+    vp[u] = V + (long)row * a.ldv + c * 8;
+    ksoff[u] = row * SK + c * 8;
+    vsoff[u] = row * SV + c * 8;
+  }
+  auto slot_ok = [&](int u) { return u < NCH - 1 || tid + 256 * u < KT * CPR; };
+  auto load = [&](int j0) {
+    const long ko = (long)j0 * a.ldk, vo = (long)j0 * a.ldv;
+    if (j0 + KT <= a.Lk) {
+#pragma unroll
+      for (int u = 0; u < NCH; ++u)
+        if (slot_ok(u)) {
+          kreg[u] = *(const uint4*)(kp[u] + ko);
+          vreg[u] = *(const uint4*)(vp[u] + vo);
         }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const bool in = j0 + krow[u] < a.Lk;
+        kreg[u] = in ? *(const uint4*)(kp[u] + ko) : make_uint4(0, 0, 0, 0);
+        vreg[u] = in ? *(const uint4*)(vp[u] + vo) : make_uint4(0, 0, 0, 0);
       }
     }
   };
-  load(0);
-
-  for (int j0 = 0; j0 < kend; j0 += KT) {
-    __syncthreads();
+  auto stage = [&](int buf) {
 #pragma unroll
-    for (int u = 0; u < NCH; ++u) {
-      const int idx = tid + 256 * u;
-      if (idx < KT * CPR) {
-        const int row = idx / CPR, c = idx - row * CPR;
-        *(uint4*)(Ks + row * SK + c * 8) = kreg[u];
-        *(uint4*)(Vs + row * SV + c * 8) = vreg[u];
+    for (int u = 0; u < NCH; ++u)
+      if (slot_ok(u)) {
+        *(uint4*)(Ks2 + buf * KT * SK + ksoff[u]) = kreg[u];
+        *(uint4*)(Vs2 + buf * KT * SV + vsoff[u]) = vreg[u];
       }
-    }
-    __syncthreads();
-    if (j0 + KT < kend) load(j0 + KT);
+  };
+  load(0);
+  __syncthreads();          // pad-column initialisation complete
+  stage(0);
+  __syncthreads();
+  if (KT < kend) load(KT);
+
+  for (int j0 = 0, it = 0; j0 < kend; j0 += KT, ++it) {
+    const uint16_t* Ks = Ks2 + (it & 1) * KT * SK;
+    const uint16_t* Vs = Vs2 + (it & 1) * KT * SV;
 
     // ---- S'^T = K Q^T - m
     f32x16 sacc[NSUB];
@@ -668,12 +689,18 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
           if (key >= a.Lk || (CAUSAL && key > qrow)) sacc[c][k] = -INFINITY;
         }
     }
-    // row max: 3-input max chains (v_max3_f32), then the other lane half
-    float tmax = fmaxf(sacc[0][0], sacc[0][1]);
+    // row max: four independent v_max3_f32 chains (short dependency chains), then the other lane half
+    float mx[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) mx[t] = fmaxf(sacc[0][4 * t], sacc[0][4 * t + 1]);
 #pragma unroll
     for (int c = 0; c < NSUB; ++c)
 #pragma unroll
-      for (int k = (c == 0 ? 2 : 0); k < 16; k += 2) tmax = fmaxf(fmaxf(tmax, sacc[c][k]), sacc[c][k + 1]);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int k = (c == 0 ? 2 : 0); k < 4; k += 2)
+          mx[t] = fmaxf(fmaxf(mx[t], sacc[c][4 * t + k]), sacc[c][4 * t + k + 1]);
+    float tmax = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
     tmax = fmaxf(tmax, xlane32(tmax));
     if (first || __any(tmax > THR)) {
       // move m (first tile: to the tile max; later: up by the excess, deferred until it passes THR)
@@ -725,6 +752,11 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
           oacc[dt] = Mfma<T>::m32x32x16(vf, pb[s2], oacc[dt]);
         }
     }
+    // tile j+1 (registers since last iteration) into the other stage, last read in iteration it-1: every wave
+    // has passed the barrier that ended it-1
+    if (j0 + KT < kend) stage((it + 1) & 1);
+    __syncthreads();
+    if (j0 + 2 * KT < kend) load(j0 + 2 * KT);
   }
 
   // ---- normalise, store O[q][h*d + e] (runs of 4 consecutive e per lane)
@@ -849,6 +881,7 @@ void attention(const AttnArgs& a, hipStream_t s) {
 }
 int g_attn_v3 = 1;
 int g_attn_xcd = 1;
+int g_attn_hm = 1;
 
 bool g_attn_v2 = true;
 int g_attn_d40 = 2;   // d = 40 variant (A/B): 0 128-key tiles (ones-column row sums), 1 VALU row sums,

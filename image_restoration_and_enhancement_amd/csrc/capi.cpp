@@ -72,6 +72,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "attn_d40") g_attn_d40 = value;
   else if (n == "attn_v3") g_attn_v3 = value;
   else if (n == "attn_xcd") g_attn_xcd = value;
+  else if (n == "attn_hm") g_attn_hm = value;
   else if (n == "gemm_small_kmax") g_gemm_small_kmax = value;
   else if (n == "nlm_strip") g_nlm_strip = value;
   else if (n == "nlm_v2") g_nlm_v2 = value;

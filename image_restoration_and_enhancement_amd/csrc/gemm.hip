@@ -25,7 +25,7 @@ struct RowInfo {   // per staged A row (conv mode)
   int iy0, ix0;    // top-left input coordinate of the receptive field
 };
 
-template <typename T, int WM, int WN, int TM, int TN, bool CONV, bool OUTF32>
+template <typename T, int WM, int WN, int TM, int TN, bool CONV, bool OUTF32, bool HS = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs a) {
   constexpr int VEC = 16 / (int)sizeof(T);      // elements per 16-byte chunk
   constexpr int BK = 8 * VEC;                   // 128-byte K step per row
@@ -213,8 +213,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs a) {
         v = apply_act(v, a.act);
         if (Rp) v += ld_f<T>(Rp + (long)m * a.ldr + n);
         v *= a.out_scale;
-        if constexpr (OUTF32) ((float*)a.C)[(long)z * a.sC + (long)m * a.ldc + n] = v;
-        else ((T*)a.C)[(long)z * a.sC + (long)m * a.ldc + n] = from_f<T>(v);
+        const long off = HS ? c_off(a, m, n) : (long)m * a.ldc + n;   // HS: head-split layout (small M only)
+        if constexpr (OUTF32) ((float*)a.C)[(long)z * a.sC + off] = v;
+        else ((T*)a.C)[(long)z * a.sC + off] = from_f<T>(v);
       }
     }
   }
@@ -235,7 +236,10 @@ void launch_cfg(const GemmArgs& a, hipStream_t s) {
   dim3 grid(tiles, a.batch), block(kThreads);
   ProfScope ps(prof_on() ? kname<T, WM, WN, TM, TN>(a.conv, a.out_f32) : std::string(),
                2.0 * a.M * a.N * (double)a.K * a.batch, s);
-  if (a.conv) {
+  if (a.hs_L) {
+    IRX_CHECK(!a.conv && !a.out_f32, "head-split output: plain 16-bit GEMMs only");
+    gemm_kernel<T, WM, WN, TM, TN, false, false, true><<<grid, block, 0, s>>>(a);
+  } else if (a.conv) {
     if (a.out_f32) gemm_kernel<T, WM, WN, TM, TN, true, true><<<grid, block, 0, s>>>(a);
     else gemm_kernel<T, WM, WN, TM, TN, true, false><<<grid, block, 0, s>>>(a);
   } else {
@@ -262,6 +266,8 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   IRX_CHECK(a.M > 0 && a.N > 0 && a.K > 0, "empty GEMM");
   IRX_CHECK(a.K % vec == 0, "K must be a multiple of 16 bytes of elements");
   IRX_CHECK(a.B && a.C, "null operand");
+  IRX_CHECK(a.hs_L == 0 || (a.batch == 1 && !a.geglu && a.hs_d % 8 == 0 && a.hs_C % a.hs_d == 0 &&
+                            a.N % a.hs_C == 0 && a.M % a.hs_L == 0), "head-split output layout");
   IRX_CHECK(a.ldb % vec == 0 && ((uintptr_t)a.B % 16) == 0, "B rows must be 16-byte aligned");
   if (a.conv) {
     const ConvGeom& g = a.g;
@@ -278,8 +284,8 @@ void gemm(const GemmArgs& a, hipStream_t s) {
     IRX_CHECK(gemm_geglu_fusable(a) && gemm_large_tile(a, s), "GEGLU epilogue needs the large-tile path");
     return;
   }
+  if (a.dtype != F32 && g_large_tiles && gemm_large_tile(a, s)) return;
   if (a.dtype == F32) launch_t<float>(a, s);
-  else if (g_large_tiles && gemm_large_tile(a, s)) return;
   else if (a.dtype == F16) launch_t<f16_t>(a, s);
   else launch_t<bf16_t>(a, s);
 }

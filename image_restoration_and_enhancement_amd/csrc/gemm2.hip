@@ -514,7 +514,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           for (int e = 0; e < 8; ++e) f[e] *= a.out_scale;
           u = Vec16<T>::pack(f);
         }
-        *(uint4*)(Cp + (long)m * a.ldc + n) = u;
+        *(uint4*)(Cp + c_off(a, m, n)) = u;
       }
       return;
     }
@@ -569,11 +569,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
     f[e] = v * a.out_scale;
   }
   if constexpr (OUTF32) {
-    float* C = (float*)a.C + (long)z * a.sC + (long)m * a.ldc + n;
+    float* C = (float*)a.C + (long)z * a.sC + c_off(a, m, n);
 #pragma unroll
     for (int e = 0; e < 8; ++e) C[e] = f[e];
   } else {
-    *(uint4*)((uint16_t*)a.C + (long)z * a.sC + (long)m * a.ldc + n) = Vec16<T>::pack(f);
+    *(uint4*)((uint16_t*)a.C + (long)z * a.sC + c_off(a, m, n)) = Vec16<T>::pack(f);
   }
 }
 
@@ -732,6 +732,7 @@ bool vec_ok(const GemmArgs& a) {
 
 bool eligible(const GemmArgs& a) {
   const int bk = step_k();
+  if (a.hs_L && !vec_ok(a)) return false;  // head-split stores: the 16-byte LDS-staged epilogue only
   if (a.act != ACT_NONE) return false;   // activations are fused by the 4-wave kernel only (tiny GEMMs)
   // the unrolled scalar (non-16-byte) epilogue only scales and adds bias: row add / residual need vec rows
   if (!vec_ok(a) && (a.rowadd || a.residual)) return false;

@@ -315,14 +315,31 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   // self-attention
   lnorm(c, h.p, M, C, a.ln1w, a.ln1b, 1e-5f, n);
   void* qkv = c.ws->alloc(M * 3 * C * es);
-  linear(c, n, C, M, C, a.qkvw, 3 * C, nullptr, qkv, 3 * C, ACT_NONE, nullptr, 0, 0, B);
+  // 16-bit engines: q|k|v written head-major ([q|k|v][image][head][token][d], GemmArgs::hs_*) so each attention
+  // block streams its head's K / V rows contiguously
+  const bool hm = dt_ != F32 && g_attn_hm;
+  {
+    GemmArgs g;
+    g.dtype = dt_; g.M = M; g.N = 3 * C; g.K = C;
+    g.A = n; g.lda = C; g.B = ptr(a.qkvw); g.ldb = C;
+    g.C = qkv; g.ldc = 3 * C; g.imgs = B;
+    if (hm) { g.hs_L = HW; g.hs_C = C; g.hs_d = d; }
+    run_gemm(c, g);
+  }
   if (!c.ws->dry()) {
     AttnArgs aa;
     aa.dtype = dt_; aa.B = B; aa.H = heads; aa.Lq = HW; aa.Lk = HW; aa.d = d; aa.scale = scale;
     aa.q_scaled = dt_ != F32;
-    aa.q = qkv; aa.ldq = 3 * C; aa.sq = (long)HW * 3 * C;
-    aa.k = (char*)qkv + C * es; aa.ldk = 3 * C; aa.sk = aa.sq;
-    aa.v = (char*)qkv + 2 * C * es; aa.ldv = 3 * C; aa.sv = aa.sq;
+    if (hm) {
+      const long hs = (long)HW * d, bs = (long)heads * hs;
+      aa.q = qkv; aa.ldq = d; aa.sq = bs; aa.hsq = hs;
+      aa.k = (char*)qkv + M * C * es; aa.ldk = d; aa.sk = bs; aa.hsk = hs;
+      aa.v = (char*)qkv + 2 * M * C * es; aa.ldv = d; aa.sv = bs; aa.hsv = hs;
+    } else {
+      aa.q = qkv; aa.ldq = 3 * C; aa.sq = (long)HW * 3 * C;
+      aa.k = (char*)qkv + C * es; aa.ldk = 3 * C; aa.sk = aa.sq;
+      aa.v = (char*)qkv + 2 * C * es; aa.ldv = 3 * C; aa.sv = aa.sq;
+    }
     aa.o = att; aa.ldo = C; aa.so = (long)HW * C;
     attention(aa, c.s);
   }
@@ -330,12 +347,20 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   linear(c, att, C, M, C, a.o1w, C, fptr(a.o1b), h.p, C, ACT_NONE, h.p, C, 0, B);
   // cross-attention (K|V precomputed per prompt)
   lnorm(c, h.p, M, C, a.ln2w, a.ln2b, 1e-5f, n);
-  linear(c, n, C, M, C, a.q2w, C, nullptr, att, C, ACT_NONE, nullptr, 0, 0, B);
+  {
+    GemmArgs g;
+    g.dtype = dt_; g.M = M; g.N = C; g.K = C;
+    g.A = n; g.lda = C; g.B = ptr(a.q2w); g.ldb = C;
+    g.C = att; g.ldc = C; g.imgs = B;
+    if (hm) { g.hs_L = HW; g.hs_C = C; g.hs_d = d; }
+    run_gemm(c, g);
+  }
   if (!c.ws->dry()) {
     AttnArgs aa;
     aa.dtype = dt_; aa.B = B; aa.H = heads; aa.Lq = HW; aa.Lk = L; aa.d = d; aa.scale = scale;
     aa.q_scaled = dt_ != F32;
-    aa.q = att; aa.ldq = C; aa.sq = (long)HW * C;
+    if (hm) { aa.q = att; aa.ldq = d; aa.sq = (long)heads * HW * d; aa.hsq = (long)HW * d; }
+    else { aa.q = att; aa.ldq = C; aa.sq = (long)HW * C; }
     aa.k = (const char*)kv + a.kv_off * es; aa.ldk = kv_cols_; aa.sk = (long)L * kv_cols_;
     aa.v = (const char*)kv + (a.kv_off + C) * es; aa.ldv = kv_cols_; aa.sv = aa.sk;
     aa.o = n; aa.ldo = C; aa.so = (long)HW * C;

@@ -42,10 +42,23 @@ struct GemmArgs {
   // GEGLU epilogue: B rows interleaved in (64 value, 64 gate) blocks (IRX_LAYOUT_*_GEGLU64); C gets N/2
   // columns h * gelu(g).  Only the large-tile path fuses it (gemm_geglu_fusable); else see geglu().
   int geglu = 0;
+  // head-split output (attention operands): columns are `parts` blocks of hs_C = heads x hs_d, rows are images of
+  // hs_L tokens; element (m, n) is stored at part * (M * hs_C) + ((image * heads + head) * hs_L + token) * hs_d + e,
+  // i.e. [part][image][head][token][e] (0: plain row-major with ldc)
+  int hs_L = 0, hs_C = 0, hs_d = 0;
   void* splitk_ws = nullptr; size_t splitk_ws_bytes = 0;   // caller workspace for split-K partials
   int dbg = 0;            // large-tile diagnostics (irx_set_option("gemm_dbg")): 1 skip epilogue, 2 skip MFMAs
 };
 constexpr int kCanonImages = 16;
+// element offset of output (m, n) in C (see GemmArgs::hs_L).  Fields passed by value: a reference to the
+// kernel-argument struct would make the compiler copy all of it to scratch.
+__host__ __device__ __forceinline__ long c_off_f(long m, int n, long ldc, int M, int hs_L, int hs_C, int hs_d) {
+  if (hs_L == 0) return m * ldc + n;
+  const int part = n / hs_C, rem = n - part * hs_C, hd = rem / hs_d, e = rem - hd * hs_d;
+  const long img = m / hs_L, tok = m - img * hs_L;
+  return (long)part * M * hs_C + ((img * (hs_C / hs_d) + hd) * hs_L + tok) * hs_d + e;
+}
+#define c_off(a, m, n) c_off_f((m), (n), (a).ldc, (a).M, (a).hs_L, (a).hs_C, (a).hs_d)
 void gemm(const GemmArgs& a, hipStream_t s);
 bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path; false if not eligible
 size_t gemm_workspace_bytes(const GemmArgs& a);           // split-K partial buffer the call will use
@@ -92,6 +105,7 @@ void attention(const AttnArgs& a, hipStream_t s);
 extern bool g_attn_v2;
 extern int g_attn_v3;    // 32x32x16 kernel for bf16 / fp16 (0: the round-1 kernels, bf16 only)
 extern int g_attn_xcd;   // 1: (batch, head) groups of q-blocks kept on one XCD (K/V shared in its L2)
+extern int g_attn_hm;    // 1: the UNet's q|k|v projections write head-major attention operands
 extern int g_attn_d40;   // bf16: 16x16x32 kernel (irx_set_option("attn_v2", 0) selects the 16x16x16 one)
 
 // ------------------------------------------------------------ elementwise / data movement

@@ -17,6 +17,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--dtypes", default="bf16,fp16")
+ap.add_argument("--only", default="", help="run only shapes whose label contains this (e.g. 'self d40 L4096')")
+ap.add_argument("--variants", default="", help="comma list of variants to run (default all)")
 a = ap.parse_args()
 dev = torch.device("cuda")
 L.load()
@@ -55,7 +57,11 @@ for dname in a.dtypes.split(","):
     for lab, B, Lq, Lk, C in [("self d40 L4096", 16, 4096, 4096, 320), ("cross d40", 16, 4096, 77, 320),
                               ("self d80 L1024", 16, 1024, 1024, 640), ("self d160 L256", 16, 256, 256, 1280),
                               ("self d40 L9216 b16", 16, 9216, 9216, 320)]:
+        if a.only and a.only not in lab:
+            continue
         vs = variants(dt, B, Lq, Lk, C)
+        if a.variants:
+            vs = {k: v for k, v in vs.items() if k in a.variants.split(",")}
         flops = 4.0 * B * Lq * Lk * C
         best = {x: 1e9 for x in vs}
         for _ in range(a.rounds):

@@ -38,17 +38,25 @@ def main():
     ap.add_argument("--mode", default="faithful", choices=["faithful", "batched"])
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--random-weights", action="store_true", help="seeded random SD-1.5 weights (smoke runs)")
+    ap.add_argument("--dtype", default=None, help="engine dtype: bf16 (default) | fp16 | fp32")
     a = ap.parse_args()
-    rank, world, local = D.init()
+    # the driver needs no data collectives (shards are independent; one closing barrier): gloo, so several
+    # ranks may also share one GPU
+    rank, world, local = D.init(backend="gloo")
     test_root, output_root = Path(a.test_root).resolve(), Path(a.output_root).resolve()
     if not test_root.exists():
         print(f"Error: Test root not found: {test_root}")
         sys.exit(1)
-    device = f"cuda:{local}" if world > 1 else "auto"
+    import torch
+    n_dev = torch.cuda.device_count()
+    device = f"cuda:{local % n_dev}" if world > 1 and n_dev else "auto"
     cfg = None
     if a.random_weights:
         rnd = {"fine_tuned_dir": "unused", "pretrained_id": "unused", "weights": "random"}
         cfg = {t: dict(rnd) for t in ("denoise", "sr", "colorize", "inpaint")}
+    if a.dtype:
+        cfg = dict(cfg or {})
+        cfg["engine"] = {"dtype": a.dtype}
     pipe = RestorationPipeline(device=device, config=cfg)
     for task, (task_list, kwargs) in TASKS.items():
         in_dir = test_root / task / a.split / "input"
