@@ -309,11 +309,13 @@ def main():
     roofline = None
     if not args.no_roofline:
         torch.cuda.synchronize()
+        graphs, eng.use_graphs = eng.use_graphs, False     # per-launch events need the eager launches
         L.profile_begin()
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
         prof = L.profile_end()
+        eng.use_graphs = graphs
         tot_ms = sum(p[2] for p in prof if p[3] > 0)
         tot_fl = sum(p[3] for p in prof)
         prof.sort(key=lambda p: -p[2])

@@ -62,6 +62,10 @@ _SIGS = {
     "irx_version": (i32, []),
     "irx_set_option": (i32, [C.c_char_p, i32]),
     "irx_profile_begin": (i32, []),
+    "irx_graph_begin": (i32, [vp]),
+    "irx_graph_end": (i32, [vp, C.POINTER(vp)]),
+    "irx_graph_launch": (i32, [vp, vp]),
+    "irx_graph_destroy": (i32, [vp]),
     "irx_profile_end": (i32, [C.POINTER(i32)]),
     "irx_profile_get": (i32, [i32, C.POINTER(C.c_char_p), C.POINTER(C.c_long), C.POINTER(C.c_double),
                               C.POINTER(C.c_double)]),
@@ -107,6 +111,8 @@ _SIGS = {
                           i64, i64, i64]),
     "irx_op_group_norm": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, vp]),
     "irx_op_group_norm_ws_bytes": (sz, [i32, i32, i32]),
+    "irx_op_gn_conv3": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp, i64,
+                              vp, vp, vp, vp]),
     "irx_op_layer_norm": (i32, [vp, i32, vp, i32, i32, f32, vp, vp, vp]),
     "irx_op_attention": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp,
                                i64, i64, f32, i32]),

@@ -64,6 +64,8 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gemm_deep") g_gemm_deep = value;
   else if (n == "gemm_dbg") g_gemm_dbg = value;
   else if (n == "gn_v2") g_gn_v2 = value != 0;
+  else if (n == "gn_fuse") g_gn_fuse = value;
+  else if (n == "vae_attn_rows") g_vae_attn_rows = value;
   else if (n == "splitk_inkernel") g_splitk_inkernel = value != 0;
   else if (n == "tile_256x320") g_tile_256x320 = value != 0;
   else if (n == "gemm_force") g_gemm_force = value;
@@ -78,6 +80,52 @@ int irx_set_option(const char* name, int value) {
   else if (n == "nlm_v2") g_nlm_v2 = value;
   else if (n == "nlm2_strip") g_nlm2_strip = value;
   else throw Error("unknown option " + n);
+  IRX_API_END
+}
+
+struct irx_graph {
+  hipGraphExec_t exec = nullptr;
+};
+
+int irx_graph_begin(void* s) {
+  IRX_API_BEGIN
+  IRX_CHECK(s, "graph capture needs a non-default stream");
+  IRX_CHECK(!prof_on(), "graph capture with the launch profiler on");
+  // relaxed: the host may allocate (torch's caching allocator) while the stream records
+  IRX_HIP(hipStreamBeginCapture(S(s), hipStreamCaptureModeRelaxed));
+  IRX_API_END
+}
+
+int irx_graph_end(void* s, irx_graph** out) {
+  IRX_API_BEGIN
+  IRX_CHECK(s && out, "null argument");
+  *out = nullptr;
+  hipGraph_t g = nullptr;
+  IRX_HIP(hipStreamEndCapture(S(s), &g));
+  IRX_CHECK(g, "empty graph capture");
+  hipGraphExec_t ex = nullptr;
+  const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  IRX_HIP(e);
+  auto* r = new irx_graph;
+  r->exec = ex;
+  *out = r;
+  IRX_API_END
+}
+
+int irx_graph_launch(irx_graph* g, void* s) {
+  IRX_API_BEGIN
+  IRX_CHECK(g && g->exec, "null graph");
+  IRX_HIP(hipGraphLaunch(g->exec, S(s)));
+  IRX_API_END
+}
+
+int irx_graph_destroy(irx_graph* g) {
+  IRX_API_BEGIN
+  if (g) {
+    if (g->exec) IRX_HIP(hipGraphExecDestroy(g->exec));
+    delete g;
+  }
   IRX_API_END
 }
 
@@ -442,6 +490,7 @@ int irx_op_conv2d(void* s, int dtype, const void* x0, const void* x1, int c0, in
   a.rowadd = rowadd; a.rowadd_ld = rowadd_ld; a.rows_per_group = ho * wo;
   a.residual = residual; a.ldr = cout;
   a.act = act;
+  a.imgs = n;   // image-indexed: the same tile / split choice as the models make for this per-image shape
   gemm(a, S(s));
   IRX_API_END
 }
@@ -471,6 +520,38 @@ int irx_op_group_norm(void* s, int dtype, const void* x0, const void* x1, int c0
   IRX_API_END
 }
 size_t irx_op_group_norm_ws_bytes(int n, int hw, int groups) { return gn_ws_bytes(n, hw, groups); }
+
+int irx_op_gn_conv3(void* s, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int h, int w,
+                    int groups, float eps, const float* gamma, const float* beta, int silu, const void* weight,
+                    const float* bias, int cout, const float* rowadd, long rowadd_ld, const void* residual,
+                    void* out, void* ws, int* fused) {
+  IRX_API_BEGIN
+  IRX_CHECK(fused, "null argument");
+  GemmArgs a;
+  a.dtype = dtype;
+  a.conv = 1;
+  a.g.src0 = x0; a.g.src1 = x1; a.g.C0 = c0; a.g.C1 = c1;
+  a.g.N = n; a.g.Hin = h; a.g.Win = w; a.g.Hv = h; a.g.Wv = w;
+  a.g.KH = 3; a.g.KW = 3; a.g.stride = 1; a.g.pad_t = 1; a.g.pad_l = 1; a.g.Ho = h; a.g.Wo = w;
+  a.M = n * h * w; a.N = cout; a.K = 9 * (c0 + c1);
+  a.B = weight; a.ldb = a.K;
+  a.C = out ? out : (void*)(uintptr_t)4096; a.ldc = cout;   // (query: an aligned stand-in, never written)
+  a.bias = bias;
+  a.rowadd = rowadd; a.rowadd_ld = rowadd_ld; a.rows_per_group = h * w;
+  a.residual = residual; a.ldr = cout;
+  a.imgs = n;
+  *fused = gemm_gn_fusable(a) ? 1 : 0;
+  if (!out) return 0;
+  IRX_CHECK(*fused, "shape does not take the GroupNorm-fused conv path");
+  IRX_CHECK(x0 && gamma && beta && weight && ws, "null buffer");
+  float2* ab = (float2*)ws;
+  void* gws = (char*)ws + (((size_t)n * (c0 + c1) * sizeof(float2) + 255) / 256 * 256);
+  group_norm_stats(dtype, x0, x1, c0, c1, n, h * w, groups, eps, gamma, beta, ab, gws, S(s));
+  a.gn_ab = ab;
+  a.gn_silu = silu;
+  gemm(a, S(s));
+  IRX_API_END
+}
 
 int irx_op_layer_norm(void* s, int dtype, const void* x, int rows, int c, float eps, const float* gamma,
                       const float* beta, void* out) {

@@ -284,6 +284,10 @@ void gemm(const GemmArgs& a, hipStream_t s) {
     IRX_CHECK(gemm_geglu_fusable(a) && gemm_large_tile(a, s), "GEGLU epilogue needs the large-tile path");
     return;
   }
+  if (a.gn_ab) {
+    IRX_CHECK(gemm_gn_fusable(a) && gemm_large_tile(a, s), "GroupNorm-fused operand needs the halo conv path");
+    return;
+  }
   if (a.dtype != F32 && g_large_tiles && gemm_large_tile(a, s)) return;
   if (a.dtype == F32) launch_t<float>(a, s);
   else if (a.dtype == F16) launch_t<f16_t>(a, s);

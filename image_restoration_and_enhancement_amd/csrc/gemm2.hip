@@ -290,12 +290,42 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         glds16_asm(src, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
       }
     };
+    // GroupNorm(+SiLU) of the conv input applied in LDS, once per landed halo slab (GemmArgs::gn_ab): the same
+    // gn_act + rounding as gn_apply_kernel, so the fused conv sees bit-identical operands.  Halo rows outside
+    // the image (zero-page fills) stay zero: the conv pads the normalised tensor.
+    const float2* gab = a.gn_ab ? a.gn_ab + (long)img * Cin : nullptr;
+    // chunk j of slab c: elements tid + NT * j; chunks [j0, j1) per call
+    auto transformH = [&](int c, int j0, int j1) {
+      uint4* hb = Hb + (c & 1) * HB_U4;
+      const int nel = min(nhi * 64, j1 * NT);
+#pragma unroll 1
+      for (int i = tid + j0 * NT; i < nel; i += NT) {
+        const int p = i / CPR;
+        const int y = y0 - 1 + (p >> lw);
+        if (y < 0 || y >= H) continue;
+        const float4* abp = (const float4*)(gab + c * BK + (((i % CPR) ^ swz(p)) * 8));
+        float f[8];
+        Vec16<T>::unpack(hb[i], f);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float4 v = abp[e];
+          f[2 * e] = gn_act(f[2 * e], v.x, v.y, a.gn_silu);
+          f[2 * e + 1] = gn_act(f[2 * e + 1], v.z, v.w, a.gn_silu);
+        }
+        hb[i] = Vec16<T>::pack(f);
+      }
+    };
     const int nk = kt1;   // (kt0 == 0)
     issueH(0);
 #pragma unroll
     for (int p = 0; p < S - 1; ++p)
       if (p < nk) issueB(p, p);
     __syncthreads();      // zero row visible
+    if (gab) {
+      wait_vm(IPB * min(S - 1, nk));                     // this wave's halo-0 pieces landed (B pieces may fly)
+      __syncthreads();
+      transformH(0, 0, 9 - S);                           // visible after the first main-loop barrier
+    }
     int st = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const int c = kt / 9, t = kt - 9 * c;
@@ -303,6 +333,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       int allow = IPB * min(S - 2, nk - 1 - kt);
       if (t >= 1 && t <= S - 1 && 9 * (c + 1) < nk) allow += hpw;
       wait_vm(__builtin_amdgcn_readfirstlane(allow));
+      if (gab) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's normalised-halo stores done
       asm volatile("s_barrier" ::: "memory");   // everyone's pieces landed; everyone finished reading kt-1
       if (kt + S - 1 < nk) issueB(kt + S - 1, st == 0 ? S - 1 : st - 1);
       if (t == 0 && 9 * (c + 1) < nk) issueH(c + 1);
@@ -341,6 +372,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
               acc[i][j] = Mfma<T>::m16x16x32(af[ss][i], bfr[ss][j], acc[i][j]);
         __builtin_amdgcn_s_setprio(0);
       }
+      // taps S..8 of slab c: slab c+1's halo has landed (waited for since tap S) -> normalise it in place, one
+      // NT-element chunk per tap behind this tap's MFMAs (the other resident wave's MFMAs hide its VALU work)
+      if (gab && t >= S && 9 * (c + 1) < nk) transformH(c + 1, t - S, t - S + 1);
       st = st + 1 == S ? 0 : st + 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -757,6 +791,13 @@ int g_conv_halo = 1;             // irx_set_option("conv_halo", m): 0 im2col wal
                                  // 1 halo tiles where the grid fills the chip, 2 wherever they fit (tests)
 int g_gemm_force = 0;            // irx_set_option("gemm_force", BM*100000 + BN*100 + splits): tuning sweeps
 
+int g_gn_fuse = 0;   // measured slower: the halo normalisation's VALU work does not hide under the MFMAs
+int halo_bn(const GemmArgs& a);
+
+bool gemm_gn_fusable(const GemmArgs& a) {
+  return g_gn_fuse && g_large_tiles && is16(a.dtype) && eligible(a) && halo_bn(a) != 0;
+}
+
 bool gemm_geglu_fusable(const GemmArgs& a) {
   if (!g_large_tiles || !a.geglu || !eligible(a) || !vec_ok(a)) return false;
   return choose(a).BM != 0;
@@ -785,12 +826,15 @@ int halo_bn(const GemmArgs& a) {
   if ((long)g.N * g.Hin * W != a.M || a.M % 256) return 0;
   const int bn = a.N % 160 == 0 ? 160 : 0;
   if (!bn || (g_conv_halo < 2 && canon_rows(a) / 256 * (a.N / bn) < kCUs)) return 0;
+  // (GroupNorm-fused operand: one 512-element chunk of the (256 + 2W) x 8 halo per tap, taps 3..8)
+  static_assert((256 + 2 * kHaloWMax) * 8 <= 512 * 6, "halo normalisation chunks");
   return bn;
 }
 
 // Returns false (caller uses the 4-wave kernel) when the shape does not fit the large-tile path.
 bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   if (!eligible(a)) return false;
+  IRX_CHECK(!a.gn_ab || halo_bn(a), "GroupNorm-fused operand needs the halo conv path");
   if (const int hbn = halo_bn(a)) {
     GemmArgs b = a;
     b.vec_epilogue = 1;

@@ -129,6 +129,12 @@ template <> struct Mfma<f16_t> {
 enum ActKind : int { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_QUICK_GELU = 3 };
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// GroupNorm application y = x * scale + shift (+ SiLU), the one definition gn_apply_kernel and the
+// GroupNorm-fused halo convolution share (bit-identical results on either path)
+__device__ __forceinline__ float gn_act(float x, float sc, float sh, int silu) {
+  const float y = fmaf(x, sc, sh);
+  return silu ? y * __builtin_amdgcn_rcpf(1.0f + __expf(-y)) : y;
+}
 __device__ __forceinline__ float apply_act(float x, int act) {
   switch (act) {
     case ACT_SILU: return silu_f(x);

@@ -89,11 +89,11 @@ Act Model::new_act(Ctx& c, int n, int h, int w, int ch) {
   return a;
 }
 
-void Model::conv2d(Ctx& c, const Act& x0, const Act* x1, P w, P b, int cout, int k, int stride, int pad_t,
-                   int pad_l, int hv, int wv, const Act& out, const float* rowadd, long rowadd_ld,
-                   const void* residual, int out_f32, int ldc) {
+static GemmArgs conv_args(int dt, const Act& x0, const Act* x1, const void* w, const float* b, int cout, int k,
+                          int stride, int pad_t, int pad_l, int hv, int wv, const Act& out, const float* rowadd,
+                          long rowadd_ld, const void* residual, int out_f32, int ldc) {
   GemmArgs a;
-  a.dtype = dt_;
+  a.dtype = dt;
   a.conv = 1;
   a.g.src0 = x0.p; a.g.C0 = x0.c;
   a.g.src1 = x1 ? x1->p : nullptr; a.g.C1 = x1 ? x1->c : 0;
@@ -103,13 +103,45 @@ void Model::conv2d(Ctx& c, const Act& x0, const Act* x1, P w, P b, int cout, int
   a.M = out.n * out.h * out.w;
   a.N = cout;
   a.K = k * k * (a.g.C0 + a.g.C1);
-  a.B = ptr(w); a.ldb = a.K;
+  a.B = w; a.ldb = a.K;
   a.C = out.p; a.ldc = ldc < 0 ? cout : ldc;
   a.out_f32 = out_f32;
-  a.bias = b.set ? fptr(b) : nullptr;
+  a.bias = b;
   a.rowadd = rowadd; a.rowadd_ld = rowadd_ld; a.rows_per_group = out.h * out.w;
   a.residual = residual; a.ldr = a.ldc;
   a.imgs = out.n;
+  return a;
+}
+
+void Model::gn_conv3(Ctx& c, const Act& x0, const Act* x1, P g, P gb, float eps, int silu, P w, P b, int cout,
+                     const Act& out, const float* rowadd, long rowadd_ld, const void* residual) {
+  const int C = x0.c + (x1 ? x1->c : 0);
+  GemmArgs a = conv_args(dt_, x0, x1, ptr(w), b.set ? fptr(b) : nullptr, cout, 3, 1, 1, 1, x0.h, x0.w, out, rowadd,
+                         rowadd_ld, residual, 0, -1);
+  if (gemm_gn_fusable(a)) {
+    float2* ab = (float2*)c.ws->alloc((size_t)x0.n * C * sizeof(float2));
+    void* ws = c.ws->alloc(gn_ws_bytes(x0.n, x0.h * x0.w, cfg_.norm_groups));
+    if (!c.ws->dry())
+      group_norm_stats(dt_, x0.p, x1 ? x1->p : nullptr, x0.c, x1 ? x1->c : 0, x0.n, x0.h * x0.w, cfg_.norm_groups,
+                       eps, fptr(g), fptr(gb), ab, ws, c.s);
+    c.ws->free(ws);
+    a.gn_ab = ab;
+    a.gn_silu = silu;
+    run_gemm(c, a);
+    c.ws->free(ab);
+    return;
+  }
+  Act n = new_act(c, x0.n, x0.h, x0.w, C);
+  gnorm(c, x0, x1, g, gb, eps, silu, n);
+  conv2d(c, n, nullptr, w, b, cout, 3, 1, 1, 1, x0.h, x0.w, out, rowadd, rowadd_ld, residual);
+  drop(c, n);
+}
+
+void Model::conv2d(Ctx& c, const Act& x0, const Act* x1, P w, P b, int cout, int k, int stride, int pad_t,
+                   int pad_l, int hv, int wv, const Act& out, const float* rowadd, long rowadd_ld,
+                   const void* residual, int out_f32, int ldc) {
+  GemmArgs a = conv_args(dt_, x0, x1, ptr(w), b.set ? fptr(b) : nullptr, cout, k, stride, pad_t, pad_l, hv, wv, out,
+                         rowadd, rowadd_ld, residual, out_f32, ldc);
   run_gemm(c, a);
 }
 
@@ -276,15 +308,9 @@ Act Unet::resnet(Ctx& c, const ResW& r, Act& x0, Act* x1, const float* tproj, fl
   const int B = x0.n, H = x0.h, W = x0.w;
   const int cin = x0.c + (x1 ? x1->c : 0);
   IRX_CHECK(cin == r.cin, "resnet channel mismatch");
-  Act gn1 = new_act(c, B, H, W, cin);
-  gnorm(c, x0, x1, r.n1w, r.n1b, eps, 1, gn1);
   Act h1 = new_act(c, B, H, W, r.cout);
-  conv2d(c, gn1, nullptr, r.c1w, r.c1b, r.cout, 3, 1, 1, 1, H, W, h1, tproj ? tproj + r.temb_off : nullptr,
-         temb_cols_);
-  drop(c, gn1);
-  Act gn2 = new_act(c, B, H, W, r.cout);
-  gnorm(c, h1, nullptr, r.n2w, r.n2b, eps, 1, gn2);
-  drop(c, h1);
+  gn_conv3(c, x0, x1, r.n1w, r.n1b, eps, 1, r.c1w, r.c1b, r.cout, h1, tproj ? tproj + r.temb_off : nullptr,
+           temb_cols_);
   Act sc;
   const void* res = x0.p;
   if (r.shortcut) {
@@ -293,8 +319,8 @@ Act Unet::resnet(Ctx& c, const ResW& r, Act& x0, Act* x1, const float* tproj, fl
     res = sc.p;
   }
   Act out = new_act(c, B, H, W, r.cout);
-  conv2d(c, gn2, nullptr, r.c2w, r.c2b, r.cout, 3, 1, 1, 1, H, W, out, nullptr, 0, res);
-  drop(c, gn2);
+  gn_conv3(c, h1, nullptr, r.n2w, r.n2b, eps, 1, r.c2w, r.c2b, r.cout, out, nullptr, 0, res);
+  drop(c, h1);
   if (r.shortcut) drop(c, sc);
   return out;
 }
@@ -586,14 +612,8 @@ Vae::Vae(const irx_model_config& cfg, int dtype) : Model(IRX_MODEL_VAE, cfg, dty
 Act Vae::resnet(Ctx& c, const ResW& r, Act& x) {
   const float eps = cfg_.norm_eps;
   const int B = x.n, H = x.h, W = x.w;
-  Act gn1 = new_act(c, B, H, W, r.cin);
-  gnorm(c, x, nullptr, r.n1w, r.n1b, eps, 1, gn1);
   Act h1 = new_act(c, B, H, W, r.cout);
-  conv2d(c, gn1, nullptr, r.c1w, r.c1b, r.cout, 3, 1, 1, 1, H, W, h1);
-  drop(c, gn1);
-  Act gn2 = new_act(c, B, H, W, r.cout);
-  gnorm(c, h1, nullptr, r.n2w, r.n2b, eps, 1, gn2);
-  drop(c, h1);
+  gn_conv3(c, x, nullptr, r.n1w, r.n1b, eps, 1, r.c1w, r.c1b, r.cout, h1);
   Act sc;
   const void* res = x.p;
   if (r.shortcut) {
@@ -602,15 +622,21 @@ Act Vae::resnet(Ctx& c, const ResW& r, Act& x) {
     res = sc.p;
   }
   Act out = new_act(c, B, H, W, r.cout);
-  conv2d(c, gn2, nullptr, r.c2w, r.c2b, r.cout, 3, 1, 1, 1, H, W, out, nullptr, 0, res);
-  drop(c, gn2);
+  gn_conv3(c, h1, nullptr, r.n2w, r.n2b, eps, 1, r.c2w, r.c2b, r.cout, out, nullptr, 0, res);
+  drop(c, h1);
   if (r.shortcut) drop(c, sc);
   return out;
 }
 
-// Mid-block single-head attention (d = 512): scores materialised per image (fp32), row softmax,
-// P V with V transposed once.  Batched MFMA GEMMs over the images.  The key axis is padded to a
-// multiple of 8 (zero probabilities / zero V^T columns) so the PV contraction stays 16-byte aligned.
+// Mid-block single-head attention (d = 512), row-blocked: V transposed once, then per block of query rows
+// (all images batched) fp32 scores S = Q K^T * C^-1/2 -> row softmax -> P V, with the score block capped
+// at kVaeScoreBytes whatever the resolution (8 x 9216^2 fp32 scores at 768^2 would be 2.7 GB).  Every row
+// is computed exactly as in one block (K-ordered MFMA sums, no split-K at K = 512 / HWp), so the result does
+// not depend on the blocking.  The key axis is padded to a multiple of 8 (zero probabilities / zero V^T
+// columns) so the PV contraction stays 16-byte aligned.
+constexpr size_t kVaeScoreBytes = 128u << 20;
+int g_vae_attn_rows = 0;   // irx_set_option("vae_attn_rows", R): force R query rows per block (tests); 0 = auto
+
 Act Vae::attn(Ctx& c, const AttW& a, Act& x) {
   const int B = x.n, HW = x.h * x.w, C = a.c;
   const int HWp = (HW + 7) / 8 * 8;
@@ -621,39 +647,42 @@ Act Vae::attn(Ctx& c, const AttW& a, Act& x) {
   void* qkv = c.ws->alloc(M * 3 * C * es);
   linear(c, gn.p, C, M, C, a.qkvw, 3 * C, fptr(a.qkvb), qkv, 3 * C, ACT_NONE, nullptr, 0, 0, B);
   drop(c, gn);
-  float* S = (float*)c.ws->alloc((size_t)B * HW * HWp * sizeof(float));
-  if (!c.ws->dry()) {
-    GemmArgs g;
-    g.dtype = dt_; g.M = HW; g.N = HW; g.K = C;
-    g.A = qkv; g.lda = 3 * C; g.sA = (long)HW * 3 * C;
-    g.B = (char*)qkv + C * es; g.ldb = 3 * C; g.sB = g.sA;
-    g.C = S; g.ldc = HWp; g.sC = (long)HW * HWp; g.out_f32 = 1;
-    g.alpha = 1.0f / std::sqrt((float)C);
-    g.batch = B;
-    g.imgs = B;
-    gemm(g, c.s);
-  }
-  void* P = c.ws->alloc((size_t)B * HW * HWp * es);
-  if (!c.ws->dry()) softmax_rows(dt_, S, HWp, B * HW, HW, P, HWp, c.s);   // writes zeros in cols [HW, HWp)
-  c.ws->free(S);
   void* VT = c.ws->alloc((size_t)B * C * HWp * es);
   if (!c.ws->dry()) {
     if (HWp != HW) IRX_HIP(hipMemsetAsync(VT, 0, (size_t)B * C * HWp * es, c.s));
     transpose2d(dt_, (char*)qkv + 2 * C * es, 3 * C, HW, C, VT, HWp, B, (long)HW * 3 * C, (long)C * HWp, c.s);
   }
-  c.ws->free(qkv);
+  // query rows per block: a multiple of 256 (whole tiles) within the score cap, or all rows
+  long rb = (long)(kVaeScoreBytes / ((size_t)B * HWp * sizeof(float))) / 256 * 256;
+  const int R = g_vae_attn_rows > 0 ? std::min(HW, g_vae_attn_rows) : (int)std::min<long>(HW, std::max<long>(256, rb));
+  float* S = (float*)c.ws->alloc((size_t)B * R * HWp * sizeof(float));
+  void* P = c.ws->alloc((size_t)B * R * HWp * es);
   void* O = c.ws->alloc(M * C * es);
-  if (!c.ws->dry()) {
+  for (int r0 = 0; r0 < HW && !c.ws->dry(); r0 += R) {
+    const int rows = std::min(R, HW - r0);
     GemmArgs g;
-    g.dtype = dt_; g.M = HW; g.N = C; g.K = HWp;
-    g.A = P; g.lda = HWp; g.sA = (long)HW * HWp;
-    g.B = VT; g.ldb = HWp; g.sB = (long)C * HWp;
-    g.C = O; g.ldc = C; g.sC = (long)HW * C;
+    g.dtype = dt_; g.M = rows; g.N = HW; g.K = C;
+    g.A = (char*)qkv + (size_t)r0 * 3 * C * es; g.lda = 3 * C; g.sA = (long)HW * 3 * C;
+    g.B = (char*)qkv + C * es; g.ldb = 3 * C; g.sB = g.sA;
+    g.C = S; g.ldc = HWp; g.sC = (long)R * HWp; g.out_f32 = 1;
+    g.alpha = 1.0f / std::sqrt((float)C);
     g.batch = B;
     g.imgs = B;
     gemm(g, c.s);
+    softmax_rows(dt_, S, HWp, B * R, HW, P, HWp, c.s);   // writes zeros in cols [HW, HWp); rows past `rows`
+                                                          // of each image hold stale scores and are never read
+    GemmArgs h;
+    h.dtype = dt_; h.M = rows; h.N = C; h.K = HWp;
+    h.A = P; h.lda = HWp; h.sA = (long)R * HWp;
+    h.B = VT; h.ldb = HWp; h.sB = (long)C * HWp;
+    h.C = (char*)O + (size_t)r0 * C * es; h.ldc = C; h.sC = (long)HW * C;
+    h.batch = B;
+    h.imgs = B;
+    gemm(h, c.s);
   }
+  c.ws->free(S);
   c.ws->free(P);
+  c.ws->free(qkv);
   c.ws->free(VT);
   Act out = new_act(c, B, x.h, x.w, C);
   linear(c, O, C, M, C, a.ow, C, fptr(a.ob), out.p, C, ACT_NONE, x.p, C, 0, B);

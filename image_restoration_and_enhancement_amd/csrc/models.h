@@ -9,6 +9,8 @@
 
 namespace irx {
 
+extern int g_vae_attn_rows;   // VAE mid-block attention: query rows per score block (0 = auto, capped bytes)
+
 // Deterministic first-fit allocator over a caller-owned workspace.  Run once with base == nullptr
 // ("dry run": no kernels launched) to size the workspace, then for real with identical calls.
 class Arena {
@@ -77,6 +79,10 @@ class Model {
               int act = ACT_NONE, const void* residual = nullptr, long ldr = 0, int out_f32 = 0, int imgs = 0);
   void run_gemm(Ctx& c, GemmArgs& a);   // allocates split-K partials from the workspace when needed
   void gnorm(Ctx& c, const Act& x0, const Act* x1, P g, P b, float eps, int silu, const Act& out);
+  // GroupNorm(+SiLU) of (x0 | x1) followed by a 3x3 / stride-1 / pad-1 conv into `out`: folded into the
+  // conv's halo operand path where it fits (gemm_gn_fusable), else a normalised copy and the plain conv
+  void gn_conv3(Ctx& c, const Act& x0, const Act* x1, P g, P gb, float eps, int silu, P w, P b, int cout,
+                const Act& out, const float* rowadd = nullptr, long rowadd_ld = 0, const void* residual = nullptr);
   void lnorm(Ctx& c, const void* x, int rows, int C, P g, P b, float eps, void* out);
 
   int kind_;

@@ -172,8 +172,12 @@ __global__ __launch_bounds__(256) void gn_stats3_kernel(const T* __restrict__ x0
 // per (image, group): fold the (chunk, slab) partials of gn_stats3 into (mean, rstd); 256 threads per
 // image, 256/G threads per group with 8 loads in flight each, shuffle-combined.  (A separate launch: an
 // in-kernel last-arriver finalize serialises ~2048 same-address arrival atomics, ~20 us at batch 16.)
+// Then every channel's scale / shift (gn_ab_store) for gn_apply_kernel or a GroupNorm-fused conv.
 __global__ __launch_bounds__(256) void gn_finalize3_kernel(const double* __restrict__ part, int nch, int G,
-                                                           double cnt, float eps, float2* __restrict__ mr) {
+                                                           double cnt, float eps, float2* __restrict__ mr, int C,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float2* __restrict__ ab) {
+  __shared__ float2 gmr[64];
   const int n = blockIdx.x, t = threadIdx.x;
   const int per = 256 / G;                 // power of two (host check)
   const int g = t / per, sub = t % per;
@@ -194,7 +198,28 @@ __global__ __launch_bounds__(256) void gn_finalize3_kernel(const double* __restr
     const double mean = a / cnt;
     double var = b / cnt - mean * mean;
     if (var < 0.0) var = 0.0;
-    mr[n * G + g] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+    const float2 r = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+    mr[n * G + g] = r;
+    gmr[g] = r;
+  }
+  __syncthreads();
+  const int cg = C / G;
+  for (int c = t; c < C; c += 256) {
+    const float2 r = gmr[c / cg];
+    const float sc = r.y * gamma[c];
+    ab[(long)n * C + c] = make_float2(sc, fmaf(-r.x, sc, beta[c]));
+  }
+}
+
+// per-channel scale / shift from (mean, rstd) (after the v1 finalize)
+__global__ __launch_bounds__(256) void gn_ab_kernel(const float2* __restrict__ mr, int G, int C,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    float2* __restrict__ ab) {
+  const int n = blockIdx.x, cg = C / G;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float2 r = mr[n * G + c / cg];
+    const float sc = r.y * gamma[c];
+    ab[(long)n * C + c] = make_float2(sc, fmaf(-r.x, sc, beta[c]));
   }
 }
 
@@ -214,29 +239,12 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const double* __restric
 
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x0, const T* __restrict__ x1, int C0,
-                                                       int C1, int HW, int G, const float2* __restrict__ mr,
-                                                       const float* __restrict__ gamma,
-                                                       const float* __restrict__ beta, int silu, T* __restrict__ out,
-                                                       int pix_per_block) {
+                                                       int C1, int HW, const float2* __restrict__ abg, int silu,
+                                                       T* __restrict__ out, int pix_per_block) {
   constexpr int VEC = 16 / (int)sizeof(T);
-  __shared__ float mean_s[64], rstd_s[64];
-  extern __shared__ float ab[];   // [2][C]
   const int C = C0 + C1;
   const int n = blockIdx.y;
-  if (threadIdx.x < G) {
-    const float2 v = mr[n * G + threadIdx.x];
-    mean_s[threadIdx.x] = v.x;
-    rstd_s[threadIdx.x] = v.y;
-  }
-  __syncthreads();
-  const int cg = C / G;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const int grp = c / cg;
-    const float sc = rstd_s[grp] * gamma[c];
-    ab[c] = sc;
-    ab[C + c] = beta[c] - mean_s[grp] * sc;
-  }
-  __syncthreads();
+  const float2* ab = abg + (long)n * C;
   // thread -> fixed 16-byte channel chunk (its scale/shift held in registers) x a pixel stride
   const int nv = C / VEC;
   const int rows = nv >= (int)blockDim.x ? 1 : blockDim.x / nv;
@@ -249,93 +257,114 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x0,
     const int c = v * VEC;
     float sc[VEC], sh[VEC];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) { sc[e] = ab[c + e]; sh[e] = ab[C + c + e]; }
+    for (int e = 0; e < VEC; ++e) { const float2 v = ab[c + e]; sc[e] = v.x; sh[e] = v.y; }
     const T* src = c < C0 ? x0 + (long)n * HW * C0 + c : x1 + (long)n * HW * C1 + (c - C0);
     const int ld = c < C0 ? C0 : C1;
     T* dst = out + (long)n * HW * C + c;
-    for (int p = p0 + r; p < p1; p += rows) {
+    auto one = [&](const uint4& u, int p) {
       float f[VEC];
-      Vec16<T>::unpack(*(const uint4*)(src + (long)p * ld), f);
+      Vec16<T>::unpack(u, f);
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        const float y = fmaf(f[e], sc[e], sh[e]);
-        f[e] = silu ? y * __builtin_amdgcn_rcpf(1.0f + __expf(-y)) : y;
-      }
+      for (int e = 0; e < VEC; ++e) f[e] = gn_act(f[e], sc[e], sh[e], silu);
       *(uint4*)(dst + (long)p * C) = Vec16<T>::pack(f);
+    };
+    int p = p0 + r;
+    for (; p + 3 * rows < p1; p += 4 * rows) {   // four 16-byte loads in flight per thread
+      const uint4 u0 = *(const uint4*)(src + (long)p * ld);
+      const uint4 u1 = *(const uint4*)(src + (long)(p + rows) * ld);
+      const uint4 u2 = *(const uint4*)(src + (long)(p + 2 * rows) * ld);
+      const uint4 u3 = *(const uint4*)(src + (long)(p + 3 * rows) * ld);
+      one(u0, p); one(u1, p + rows); one(u2, p + 2 * rows); one(u3, p + 3 * rows);
     }
+    for (; p < p1; p += rows) one(*(const uint4*)(src + (long)p * ld), p);
   }
 }
 
-// LayerNorm: one wave per row, row held in registers, two-pass mean/var in fp32.
-template <typename T, int MAXV>
+// LayerNorm: one wave per row, row held in registers, two-pass mean/var in fp32.  RPW rows per wave with all
+// of their 16-byte loads issued before the first row's reductions (more bytes in flight per wave).
+template <typename T, int MAXV, int RPW>
 __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long ldx, int rows, int C, float eps,
                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
                                                  T* __restrict__ out, long ldo) {
   constexpr int VEC = 16 / (int)sizeof(T);
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= rows) return;
   const int nv = C / VEC;
-  float f[MAXV][VEC];
-  float s = 0.f;
+  uint4 raw[RPW][MAXV];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int v = lane + 64 * i;
-    if (v < nv) {
-      Vec16<T>::unpack(*(const uint4*)(x + (long)row * ldx + v * VEC), f[i]);
+  for (int k = 0; k < RPW; ++k)
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) s += f[i][e];
+    for (int i = 0; i < MAXV; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nv && row0 + k < rows) raw[k][i] = *(const uint4*)(x + (long)(row0 + k) * ldx + v * VEC);
     }
-  }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  const float mean = s / C;
-  float q = 0.f;
+  for (int k = 0; k < RPW; ++k) {
+    const int row = row0 + k;
+    if (row >= rows) break;
+    float f[MAXV][VEC];
+    float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int v = lane + 64 * i;
-    if (v < nv) {
+    for (int i = 0; i < MAXV; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nv) {
+        Vec16<T>::unpack(raw[k][i], f[i]);
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) { const float dd = f[i][e] - mean; q += dd * dd; }
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
-  const float rstd = rsqrtf(q / C + eps);
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int v = lane + 64 * i;
-    if (v < nv) {
-      float y[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        const int c = v * VEC + e;
-        y[e] = (f[i][e] - mean) * rstd * gamma[c] + beta[c];
+        for (int e = 0; e < VEC; ++e) s += f[i][e];
       }
-      *(uint4*)(out + (long)row * ldo + v * VEC) = Vec16<T>::pack(y);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nv) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) { const float dd = f[i][e] - mean; q += dd * dd; }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    const float rstd = rsqrtf(q / C + eps);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int v = lane + 64 * i;
+      if (v < nv) {
+        float y[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const int c = v * VEC + e;
+          y[e] = (f[i][e] - mean) * rstd * gamma[c] + beta[c];
+        }
+        *(uint4*)(out + (long)row * ldo + v * VEC) = Vec16<T>::pack(y);
+      }
     }
   }
 }
 
+constexpr int kMaxC = 8192;
+
+// statistics of the (two-source) tensor -> per-channel scale / shift `ab` [N][C]
 template <typename T>
-void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps, const float* gamma,
-          const float* beta, int silu, void* out, void* ws, hipStream_t s) {
+void gn_stats_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps, const float* gamma,
+                const float* beta, float2* ab, void* ws, hipStream_t s) {
   const int nch = n_chunks(HW);
   double* part = (double*)ws;
   float2* mr = (float2*)(part + (size_t)N * kMaxChunks * G * 2);
   const int C = C0 + C1;
   const int VEC = 16 / (int)sizeof(T);
-  const int nvv = C / VEC;
-  const int rws = nvv >= 256 ? 1 : 256 / nvv;
   const int slabs = gn_slabs(C, VEC, G);
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_stats3_kernel") : std::string(), 0.0, s);
   if (g_gn_v2 && N <= 4096 && slabs > 0) {
-    ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_stats3_kernel") : std::string(), 0.0, s);
     const int rows3 = 256 / (C / slabs / VEC);
     const int nch3 = gn_chunks3(HW, slabs, rows3);
     gn_stats3_kernel<T><<<dim3(nch3, N, slabs), 256, 0, s>>>(
         (const T*)x0, (const T*)x1, C0, C1, HW, G, (HW + nch3 - 1) / nch3, part);
     IRX_LAUNCH_CHECK();
-    gn_finalize3_kernel<<<N, 256, 0, s>>>(part, nch3, G, (double)HW * (C / G), eps, mr);
+    gn_finalize3_kernel<<<N, 256, 0, s>>>(part, nch3, G, (double)HW * (C / G), eps, mr, C, gamma, beta, ab);
     IRX_LAUNCH_CHECK();
   } else {
     gn_stats_kernel<T><<<dim3(nch, N), 256, 0, s>>>((const T*)x0, (const T*)x1, C0, C1, HW, G, chunk_pix(HW),
@@ -343,16 +372,32 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
     IRX_LAUNCH_CHECK();
     gn_finalize_kernel<<<N, 64, 0, s>>>(part, nch, G, (double)HW * (C / G), eps, mr);
     IRX_LAUNCH_CHECK();
+    gn_ab_kernel<<<N, 256, 0, s>>>(mr, G, C, gamma, beta, ab);
+    IRX_LAUNCH_CHECK();
   }
+}
+
+float2* gn_ab_ws(void* ws, int N, int G) {
+  return (float2*)((char*)ws + (size_t)N * kMaxChunks * G * 2 * sizeof(double) + (size_t)N * G * sizeof(float2));
+}
+
+template <typename T>
+void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps, const float* gamma,
+          const float* beta, int silu, void* out, void* ws, hipStream_t s) {
+  float2* ab = gn_ab_ws(ws, N, G);
+  gn_stats_t<T>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, ab, ws, s);
+  const int C = C0 + C1;
+  const int VEC = 16 / (int)sizeof(T);
   // ~16 pixels per thread per block, one fixed channel chunk per thread
   const int nv = C / VEC;
   const int rows = nv >= 256 ? 1 : 256 / nv;
   // pixels per thread: up to 16, fewer when the tensor is small, so the grid still has ~2048 blocks
-  const int ppt = std::max(1, std::min(16, (int)((long)N * HW / ((long)rows * 2048))));
+  int ppt = std::max(1, std::min(16, (int)((long)N * HW / ((long)rows * 2048))));
+  if (ppt >= 4) ppt &= ~3;   // whole groups of four loads in flight
   const int ppb = rows * ppt;
   ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_apply_kernel") : std::string(), 0.0, s);
-  gn_apply_kernel<T><<<dim3((HW + ppb - 1) / ppb, N), 256, 2 * C * sizeof(float), s>>>(
-      (const T*)x0, (const T*)x1, C0, C1, HW, G, mr, gamma, beta, silu, (T*)out, ppb);
+  gn_apply_kernel<T><<<dim3((HW + ppb - 1) / ppb, N), 256, 0, s>>>((const T*)x0, (const T*)x1, C0, C1, HW, ab, silu,
+                                                                  (T*)out, ppb);
   IRX_LAUNCH_CHECK();
 }
 
@@ -361,13 +406,23 @@ void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamm
           long ldo, hipStream_t s) {
   const int VEC = 16 / (int)sizeof(T);
   const int nv = C / VEC;
-  dim3 grid((rows + 3) / 4), block(256);
+  dim3 block(256);
   ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::ln_kernel") : std::string(), 0.0, s);
-  if (nv <= 64) ln_kernel<T, 1><<<grid, block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
-  else if (nv <= 128) ln_kernel<T, 2><<<grid, block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
-  else if (nv <= 256) ln_kernel<T, 4><<<grid, block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
-  else if (nv <= 512) ln_kernel<T, 8><<<grid, block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
-  else throw Error("layer_norm: C too large");
+  // rows per wave: 4 while the row is <= 2 vectors per lane (fill the chip first: >= ~2048 blocks), else 2 / 1
+  auto grid = [&](int rpw) { return dim3((rows + 4 * rpw - 1) / (4 * rpw)); };
+  if (nv <= 64) {
+    if (rows >= 4 * 4 * 2048) ln_kernel<T, 1, 4><<<grid(4), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
+    else ln_kernel<T, 1, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
+  } else if (nv <= 128) {
+    if (rows >= 4 * 2 * 2048) ln_kernel<T, 2, 2><<<grid(2), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
+    else ln_kernel<T, 2, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
+  } else if (nv <= 256) {
+    ln_kernel<T, 4, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
+  } else if (nv <= 512) {
+    ln_kernel<T, 8, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
+  } else {
+    throw Error("layer_norm: C too large");
+  }
   IRX_LAUNCH_CHECK();
 }
 
@@ -376,8 +431,9 @@ void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamm
 bool g_gn_v2 = true;   // irx_set_option("gn_v2", 0): v1 LDS-atomic stats + separate finalize (A/B)
 
 size_t gn_ws_bytes(int N, int HW, int G) {
-  (void)HW;   // partials for up to kMaxChunks chunks per image (v1 and v3 layouts)
-  return (size_t)N * kMaxChunks * G * 2 * sizeof(double) + (size_t)N * G * sizeof(float2);
+  (void)HW;   // partials for up to kMaxChunks chunks per image (v1 and v3 layouts), (mean, rstd), scale / shift
+  return (size_t)N * kMaxChunks * G * 2 * sizeof(double) + (size_t)N * G * sizeof(float2) +
+         (size_t)N * kMaxC * sizeof(float2);
 }
 
 void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
@@ -391,6 +447,17 @@ void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N
   if (dtype == F32) gn_t<float>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s);
   else if (dtype == F16) gn_t<f16_t>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s);
   else gn_t<bf16_t>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s);
+}
+
+void group_norm_stats(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
+                      const float* gamma, const float* beta, float2* ab, void* ws, hipStream_t s) {
+  const int vec = dtype == F32 ? 4 : 8;
+  IRX_CHECK(G > 0 && G <= 64 && (C0 + C1) % G == 0, "GroupNorm: C must divide into <= 64 groups");
+  IRX_CHECK(C0 % vec == 0 && C1 % vec == 0 && C0 + C1 <= kMaxC, "GroupNorm: channel counts");
+  IRX_CHECK(C1 == 0 || x1, "GroupNorm: concat source missing");
+  if (dtype == F32) gn_stats_t<float>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, ab, ws, s);
+  else if (dtype == F16) gn_stats_t<f16_t>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, ab, ws, s);
+  else gn_stats_t<bf16_t>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, ab, ws, s);
 }
 
 void layer_norm(int dtype, const void* x, long ldx, int rows, int C, float eps, const float* gamma,

@@ -46,6 +46,10 @@ struct GemmArgs {
   // hs_L tokens; element (m, n) is stored at part * (M * hs_C) + ((image * heads + head) * hs_L + token) * hs_d + e,
   // i.e. [part][image][head][token][e] (0: plain row-major with ldc)
   int hs_L = 0, hs_C = 0, hs_d = 0;
+  // GroupNorm(+SiLU) applied to the conv's A operand on the fly (halo path only, gemm_gn_fusable): source
+  // channel c of image n becomes gn_act(x, gn_ab[n][c].x, gn_ab[n][c].y, gn_silu); c indexes the C0 + C1
+  // concat.  Zero padding stays zero (it pads the normalised tensor, as in the unfused form).
+  const float2* gn_ab = nullptr; int gn_silu = 0;
   void* splitk_ws = nullptr; size_t splitk_ws_bytes = 0;   // caller workspace for split-K partials
   int dbg = 0;            // large-tile diagnostics (irx_set_option("gemm_dbg")): 1 skip epilogue, 2 skip MFMAs
 };
@@ -63,6 +67,8 @@ void gemm(const GemmArgs& a, hipStream_t s);
 bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path; false if not eligible
 size_t gemm_workspace_bytes(const GemmArgs& a);           // split-K partial buffer the call will use
 bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can apply the GEGLU epilogue
+bool gemm_gn_fusable(const GemmArgs& a);                  // conv can apply GemmArgs::gn_ab to its operand
+extern int g_gn_fuse;      // 1: GroupNorm(+SiLU) folded into the following halo conv where it fits (0: A/B)
 extern bool g_large_tiles;
 extern int g_gemm_deep;    // large-tile pipeline: 0 two-stage BK 64, 1 BK-32 S-stage ring, 2 BK-64 deeper ring
 extern int g_gemm_dbg;     // timing diagnostics only: results are wrong when set
@@ -80,6 +86,10 @@ extern int g_conv_halo;      // 3x3 convs on whole-row tiles: one LDS halo per 3
 extern bool g_gn_v2;       // GroupNorm stats v3 (slabbed grid + finalize kernel); 0 = v1 (A/B)
 void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
                 const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s);
+// statistics only: per (image, channel) scale / shift (gamma * rstd, beta - mean * gamma * rstd) into
+// `ab` [N][C0 + C1] (float2), for a consumer that applies them itself (GemmArgs::gn_ab)
+void group_norm_stats(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
+                      const float* gamma, const float* beta, float2* ab, void* ws, hipStream_t s);
 void layer_norm(int dtype, const void* x, long ldx, int rows, int C, float eps, const float* gamma,
                 const float* beta, void* out, long ldo, hipStream_t s);
 

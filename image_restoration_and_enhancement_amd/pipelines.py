@@ -16,6 +16,7 @@ pipeline once per image.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 from pathlib import Path
 from typing import Dict, List, Optional, Sequence
@@ -80,6 +81,18 @@ class SDEngine:
         tok_dir = Path(cfg.model_dir) / "tokenizer" if cfg.model_dir else None
         self.tokenizer = PromptTokenizer(tok_dir)
         self._ctx_cache: Dict[tuple, torch.Tensor] = {}
+        # HIP-graph replay of repeated denoising loops (IRX_GRAPHS=0 disables)
+        self.use_graphs = os.environ.get("IRX_GRAPHS", "1") != "0" and self.device.type == "cuda"
+        self._graphs: Dict[tuple, dict] = {}
+        self._graph_seen: set = set()
+        self._graph_stream = torch.cuda.Stream(self.device) if self.use_graphs else None
+
+    def __del__(self):
+        for g in getattr(self, "_graphs", {}).values():
+            try:
+                L.load().irx_graph_destroy(g["exec"])
+            except Exception:
+                pass
 
     # ------------------------------------------------------------------ weights
     def _load_weights(self, weights, seed):
@@ -138,21 +151,84 @@ class SDEngine:
         L.call("irx_tensor_to_image", _stream(), self.dt, _p(img), B, H, W_, 4, _p(u8), _p(f01))
         return u8, f01
 
+    def _loop_buffers(self, lat: torch.Tensor, plans: List[StepPlan], cfg_on: bool) -> dict:
+        B, h, w, _ = lat.shape
+        UB = 2 * B if cfg_on else B
+        n_slots = max([(-1 if p.store_slot is None else p.store_slot) for p in plans] + [-1]) + 1
+        return {
+            "x_in": torch.empty((UB, h, w, self.unet.cin_pad), dtype=self.tdt, device=self.device),
+            "eps": torch.empty((UB, h, w, 4), dtype=torch.float32, device=self.device),
+            "slots": [torch.empty_like(lat) for _ in range(n_slots)],
+            "cur": torch.empty_like(lat) if any(p.save_cur for p in plans) else None,
+            "t_all": torch.tensor([[float(p.t)] * UB for p in plans], dtype=torch.float32).to(self.device),
+        }
+
     def denoise_loop(self, lat: torch.Tensor, kv: torch.Tensor, plans: List[StepPlan], guidance: float,
                      cfg_on: bool, mask_l: Optional[torch.Tensor] = None,
                      masked_l: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The denoising loop.  With `use_graphs`, the second call of an identical loop (shapes, plans, guidance)
+        records it as one HIP graph (irx_graph_*) on the engine's stream and every later call replays it into
+        persistent buffers: ~600 launches per UNet eval issued by one hipGraphLaunch."""
+        if not self.use_graphs or not lat.is_cuda:
+            return self._loop_body(lat, kv, plans, guidance, cfg_on, mask_l, masked_l,
+                                   self._loop_buffers(lat, plans, cfg_on))
+        key = (tuple(lat.shape), tuple(kv.shape), bool(cfg_on), float(guidance), mask_l is not None,
+               tuple((p.t, p.mode, tuple(p.c), tuple(p.hw), p.e_div, p.e_mul, p.store_slot, tuple(p.hist),
+                      p.x_from_cur, p.save_cur) for p in plans))
+        cs = torch.cuda.current_stream(self.device)
+        gs = self._graph_stream
+        gs.wait_stream(cs)
+        with torch.cuda.stream(gs):
+            g = self._graphs.get(key)
+            if g is None and key not in self._graph_seen:
+                # first sight: eager on the graph stream (sizes the workspaces, creates its split-K tickets)
+                self._graph_seen.add(key)
+                out = self._loop_body(lat, kv, plans, guidance, cfg_on, mask_l, masked_l,
+                                      self._loop_buffers(lat, plans, cfg_on))
+            else:
+                if g is None:
+                    g = self._capture(key, lat, kv, plans, guidance, cfg_on, mask_l, masked_l)
+                g["lat"].copy_(lat)
+                g["kv"].copy_(kv)
+                if mask_l is not None:
+                    g["mask"].copy_(mask_l)
+                    g["masked"].copy_(masked_l)
+                L.call("irx_graph_launch", g["exec"], _stream())
+                out = g["lat"].clone()
+        cs.wait_stream(gs)
+        return out
+
+    def _capture(self, key, lat, kv, plans, guidance, cfg_on, mask_l, masked_l) -> dict:
+        g = {"lat": torch.empty_like(lat), "kv": torch.empty_like(kv),
+             "mask": torch.empty_like(mask_l) if mask_l is not None else None,
+             "masked": torch.empty_like(masked_l) if masked_l is not None else None,
+             "bufs": self._loop_buffers(lat, plans, cfg_on)}
+        h = C.c_void_p()
+        L.call("irx_graph_begin", _stream())
+        try:
+            self._loop_body(g["lat"], g["kv"], plans, guidance, cfg_on, g["mask"], g["masked"], g["bufs"])
+        except BaseException:
+            L.load().irx_graph_end(_stream(), C.byref(h))   # leave capture mode, drop the partial graph
+            if h.value:
+                L.call("irx_graph_destroy", h)
+            raise
+        L.call("irx_graph_end", _stream(), C.byref(h))
+        g["exec"] = h
+        g["ws"] = self.unet._ws          # the workspace the graph's launches point into stays alive with it
+        while len(self._graphs) >= 4:                         # a few loop shapes per engine
+            old = self._graphs.pop(next(iter(self._graphs)))
+            L.call("irx_graph_destroy", old["exec"])
+        self._graphs[key] = g
+        return g
+
+    def _loop_body(self, lat, kv, plans, guidance, cfg_on, mask_l, masked_l, bufs) -> torch.Tensor:
         B, h, w, _ = lat.shape
         UB = 2 * B if cfg_on else B
         inpaint = int(mask_l is not None)
         cp = self.unet.cin_pad
-        x_in = torch.empty((UB, h, w, cp), dtype=self.tdt, device=self.device)
+        x_in, eps, slots, cur, t_all = bufs["x_in"], bufs["eps"], bufs["slots"], bufs["cur"], bufs["t_all"]
         L.call("irx_pack_unet_input", _stream(), self.dt, _p(lat), B, h, w, int(cfg_on), cp, inpaint, _p(mask_l),
                _p(masked_l), _p(x_in))
-        eps = torch.empty((UB, h, w, 4), dtype=torch.float32, device=self.device)
-        n_slots = max([(-1 if p.store_slot is None else p.store_slot) for p in plans] + [-1]) + 1
-        slots = [torch.empty_like(lat) for _ in range(n_slots)]
-        cur = torch.empty_like(lat) if any(p.save_cur for p in plans) else None
-        t_all = torch.tensor([[float(p.t)] * UB for p in plans], dtype=torch.float32).to(self.device)
         for i, p in enumerate(plans):
             self.unet.forward(x_in, t_all[i], kv, 77, out=eps)
             sp = L.StepParams()

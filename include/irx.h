@@ -86,6 +86,16 @@ int irx_profile_begin(void);
 int irx_profile_end(int* n_kernels);   /* synchronises, aggregates per kernel instantiation */
 int irx_profile_get(int i, const char** name, long* launches, double* total_ms, double* total_flops);
 
+/* ---- HIP-graph capture of a launch sequence (the denoising loop: every UNet eval + fused step kernel).
+   begin/end bracket ordinary irx calls on `stream` (a non-default stream; the calls are recorded, not run);
+   end instantiates an executable graph, launch replays it on a stream, destroy frees it.  Buffers, shapes
+   and scalar arguments are baked in at capture: replay re-runs exactly the recorded launches. ---- */
+typedef struct irx_graph irx_graph;
+int irx_graph_begin(void* stream);
+int irx_graph_end(void* stream, irx_graph** out);
+int irx_graph_launch(irx_graph* g, void* stream);
+int irx_graph_destroy(irx_graph* g);
+
 /* ---- model lifetime: replaces diffusers/transformers from_pretrained (src/inference.py:162-172) ---- */
 int irx_model_create(int kind, const irx_model_config* cfg, int dtype, irx_model** out);
 int irx_model_destroy(irx_model* m);
@@ -209,6 +219,14 @@ int irx_op_gemm(void* stream, int dtype, int M, int N, int K, const void* A, lon
 int irx_op_group_norm(void* stream, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hw,
                       int groups, float eps, const float* gamma, const float* beta, int silu, void* out, void* ws);
 size_t irx_op_group_norm_ws_bytes(int n, int hw, int groups);
+/* GroupNorm(+SiLU) of (x0 | x1) folded into a 3x3 / stride-1 / pad-1 conv's halo operand path (the form the
+   UNet / VAE resnets run); bias / rowadd / residual as irx_op_conv2d.  Fails (IRX error) when the shape does
+   not take the fused path: *fused reports whether it would (query with out == NULL, nothing launched).
+   ws: irx_op_group_norm_ws_bytes + n * (c0 + c1) * 8 bytes. */
+int irx_op_gn_conv3(void* stream, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int h, int w,
+                    int groups, float eps, const float* gamma, const float* beta, int silu, const void* weight,
+                    const float* bias, int cout, const float* rowadd, long rowadd_ld, const void* residual,
+                    void* out, void* ws, int* fused);
 int irx_op_layer_norm(void* stream, int dtype, const void* x, int rows, int c, float eps, const float* gamma,
                       const float* beta, void* out);
 int irx_op_attention(void* stream, int dtype, int batch, int heads, int lq, int lk, int d, const void* q, long ldq,

@@ -73,6 +73,31 @@ def group_norm(x0, gamma, beta, eps, groups=32, silu=False, x1=None):
     return out
 
 
+def gn_conv3(x0, gamma, beta, eps, w_oihw, bias, groups=32, silu=True, x1=None, rowadd=None, residual=None,
+             query=False):
+    """GroupNorm(+SiLU) folded into the halo 3x3 conv (irx_op_gn_conv3); query=True only reports whether the
+    shape takes the fused path."""
+    import ctypes
+    N, H, W, C0 = x0.shape
+    C1 = x1.shape[3] if x1 is not None else 0
+    Co = w_oihw.shape[0]
+    fused = ctypes.c_int(0)
+    if query:
+        L.call("irx_op_gn_conv3", S(), DT[x0.dtype], None, None, C0, C1, N, H, W, groups, float(eps), None, None,
+               int(silu), None, None, Co, None, 0, None, None, None, ctypes.byref(fused))
+        return bool(fused.value)
+    wk = w_oihw.permute(0, 2, 3, 1).contiguous().to(device=x0.device, dtype=x0.dtype)
+    b = bias.float().to(x0.device).contiguous() if bias is not None else None
+    nb = L.load().irx_op_group_norm_ws_bytes(N, H * W, groups) + N * (C0 + C1) * 8 + 256
+    ws = torch.empty(nb, dtype=torch.uint8, device=x0.device)
+    out = torch.empty((N, H, W, Co), dtype=x0.dtype, device=x0.device)
+    L.call("irx_op_gn_conv3", S(), DT[x0.dtype], P(x0), P(x1), C0, C1, N, H, W, groups, float(eps), P(gamma),
+           P(beta), int(silu), P(wk), P(b), Co, P(rowadd), rowadd.shape[1] if rowadd is not None else 0,
+           P(residual), P(out), P(ws), ctypes.byref(fused))
+    assert fused.value == 1
+    return out
+
+
 def layer_norm(x, gamma, beta, eps):
     rows, Cc = x.shape
     out = torch.empty_like(x)

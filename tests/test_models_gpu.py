@@ -176,3 +176,29 @@ def test_batch_shares_noise(device):
         one = eng.img2img(torch.from_numpy(imgs[i:i + 1]).to(device).contiguous(), prompt, strength, steps,
                           guidance, n_evals=2).images_u8.cpu()
         assert torch.equal(one[0], batch[i])
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_vae_attention_row_blocks_bit_exact(device, denoise_sd, dtype):
+    """The VAE mid-block attention runs in blocks of query rows (bounded score memory at 768^2); the blocking
+    must not change a single bit: 4 blocks of 256 rows vs one block of L = 1024 rows, encode and decode."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    from image_restoration_and_enhancement_amd.engine import VAE, TORCH_DT, dtype_code
+    pc, sd = denoise_sd
+    tdt = TORCH_DT[dtype_code(dtype)]
+    vae = VAE(pc.vae, dtype, device)
+    vae.load_state_dict(sd["vae"])
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(2, 256, 256, 8, generator=g) * 2 - 1)
+    x[..., 3:] = 0
+    z = torch.randn(2, 32, 32, 8, generator=g)
+    x, z = x.to(tdt).to(device).contiguous(), z.to(tdt).to(device).contiguous()
+    outs = []
+    for rows in (0, 256):
+        L.call("irx_set_option", b"vae_attn_rows", rows)
+        try:
+            outs.append((vae.encode(x).clone(), vae.decode(z).clone()))
+        finally:
+            L.call("irx_set_option", b"vae_attn_rows", 0)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -360,6 +360,76 @@ def test_conv_halo(device, halo_forced, case, dt):
     assert O.rel_err(got, ref) < TOL[dt]
 
 
+@pytest.mark.parametrize("case", [
+    # (N, H, W, C0, C1, Cout, rowadd+residual, forced): the UNet resnet shapes that take the fused path at
+    # batch 16, and small forced-halo shapes (concat seam inside a group, W 16 / 32 / 64)
+    (2, 64, 64, 320, 0, 320, False, False),
+    (1, 64, 64, 640, 320, 320, True, False),   # up-block concat (groups of 30 straddle the seam) + temb + residual
+    (1, 32, 32, 1280, 640, 640, True, False),
+    (2, 16, 32, 128, 64, 160, True, True),
+    (1, 16, 16, 64, 64, 160, False, True),
+])
+@pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("silu", [True, False])
+def test_gn_conv3_fused_bit_exact(device, case, dt, silu):
+    """GroupNorm(+SiLU) folded into the halo conv == group_norm op then conv op, bit for bit (same per-channel
+    scale / shift, same gn_act, same rounding of the normalised operand); and both within tolerance of the
+    fp32 CPU reference."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    N, H, W, C0, C1, Co, extra, forced = case
+    L.call("irx_set_option", b"gn_fuse", 1)     # (off by default: measured slower, DESIGN §4)
+    if forced:
+        L.call("irx_set_option", b"conv_halo", 2)
+    try:
+        x0 = _r(N, H, W, C0, seed=90, scale=2.0) + 0.7
+        x1 = _r(N, H, W, C1, seed=91) - 0.3 if C1 else None
+        g = _r(C0 + C1, seed=92) * 0.2 + 1.0
+        bt = _r(C0 + C1, seed=93) * 0.1
+        w = _r(Co, C0 + C1, 3, 3, seed=94, scale=1 / math.sqrt((C0 + C1) * 9))
+        b = _r(Co, seed=95)
+        temb = _r(N, Co, seed=96).to(device).contiguous() if extra else None
+        res = _dev(_r(N, H, W, Co, seed=97), dt, device) if extra else None
+        d0 = _dev(x0, dt, device)
+        d1 = _dev(x1, dt, device) if C1 else None
+        gd, bd = g.to(device).contiguous(), bt.to(device).contiguous()
+        assert O.gn_conv3(d0, gd, bd, 1e-5, w, b, x1=d1, silu=silu, query=True)
+        got = O.gn_conv3(d0, gd, bd, 1e-5, w, b, x1=d1, silu=silu, rowadd=temb, residual=res)
+        n = O.group_norm(d0, gd, bd, 1e-5, 32, silu, x1=d1)
+        ref_dev = O.conv2d(n, w.to(dt).float(), b, rowadd=temb, residual=res)   # the same halo walk, unfused
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref_dev)
+        xin = torch.cat([_q(x0, dt)] + ([_q(x1, dt)] if C1 else []), 3).permute(0, 3, 1, 2)
+        nr = F.group_norm(xin, 32, g, bt, 1e-5)
+        nr = _q(F.silu(nr) if silu else nr, dt)
+        ref = F.conv2d(nr, _q(w, dt), b, padding=1)
+        if extra:
+            ref = ref + temb.cpu()[:, :, None, None]
+        ref = ref.permute(0, 2, 3, 1)
+        if extra:
+            ref = ref + res.cpu().float()
+        assert O.rel_err(got, ref) < TOL[dt]
+    finally:
+        L.call("irx_set_option", b"conv_halo", 1)
+        L.call("irx_set_option", b"gn_fuse", 0)
+
+
+def test_gn_conv3_not_fusable_is_refused(device):
+    """Shapes off the halo path (16x16 level at batch 2, odd widths) report fused = 0 and the launch fails loudly
+    (the models fall back to a normalised copy + plain conv)."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    dt = torch.bfloat16
+    x = _dev(_r(2, 16, 16, 1280, seed=98), dt, device)
+    g = torch.ones(1280, device=device)
+    w = _r(1280, 1280, 3, 3, seed=99, scale=0.01)
+    L.call("irx_set_option", b"gn_fuse", 1)
+    try:
+        assert not O.gn_conv3(x, g, g, 1e-5, w, None, query=True)
+        with pytest.raises(L.IrxError):
+            O.gn_conv3(x, g, g, 1e-5, w, None)
+    finally:
+        L.call("irx_set_option", b"gn_fuse", 0)
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("B,Lq,Lk", [(2, 256, 256), (2, 200, 77), (1, 333, 190)])
 def test_attention_d40_variants(device, variant, B, Lq, Lk):
