@@ -284,6 +284,10 @@ void gemm(const GemmArgs& a, hipStream_t s) {
     IRX_CHECK(gemm_geglu_fusable(a) && gemm_large_tile(a, s), "GEGLU epilogue needs the large-tile path");
     return;
   }
+  if (a.gn_part) {
+    IRX_CHECK(gemm_emits_gn_parts(a) > 0 && gemm_large_tile(a, s), "GroupNorm partials need the large-tile epilogue");
+    return;
+  }
   if (a.gn_ab) {
     IRX_CHECK(gemm_gn_fusable(a) && gemm_large_tile(a, s), "GroupNorm-fused operand needs the halo conv path");
     return;

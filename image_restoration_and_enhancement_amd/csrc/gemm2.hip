@@ -524,6 +524,122 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         }
         return;
       }
+      // one 16-byte output chunk: its operands (staged tile, residual, row add) fetched first, then the final
+      // value (row add, residual, output scale) formed and stored — split so two rows' loads overlap
+      struct Src { uint4 u, r; float4 x, y; };
+      auto fetch = [&](int row, int c, Src& q) {
+        const int m = m0 + row, n = n0 + c * 8;
+        q.u = *(const uint4*)(tileS + row * BN + (csw(c, row) << 3));
+        if (Rp) q.r = *(const uint4*)(Rp + (long)m * a.ldr + n);
+        if (a.rowadd) {
+          const float4* ra = (const float4*)(a.rowadd + (long)(m / a.rows_per_group) * a.rowadd_ld + n);
+          q.x = ra[0];
+          q.y = ra[1];
+        }
+      };
+      auto combine = [&](int row, int c, const Src& q) -> uint4 {
+        const int m = m0 + row, n = n0 + c * 8;
+        uint4 u = q.u;
+        if (Rp || a.rowadd || a.out_scale != 1.f) {
+          float f[8];
+          Vec16<T>::unpack(u, f);
+          if (a.rowadd) {
+            f[0] += q.x.x; f[1] += q.x.y; f[2] += q.x.z; f[3] += q.x.w;
+            f[4] += q.y.x; f[5] += q.y.y; f[6] += q.y.z; f[7] += q.y.w;
+          }
+          if (Rp) {
+            float rv[8];
+            Vec16<T>::unpack(q.r, rv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] += rv[e];
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] *= a.out_scale;
+          u = Vec16<T>::pack(f);
+        }
+        *(uint4*)(Cp + c_off(a, m, n)) = u;
+        return u;
+      };
+      if (a.gn_part) {
+        // GroupNorm partials of the stored output, one per tile row block of BM rows (host: gemm_emits_gn_parts):
+        // thread = fixed 8-channel chunk column x a row stride, shifted fp32 sums of the rounded values -> raw
+        // fp64 (sum, sum of squares), folded over the row groups through LDS in a fixed order.
+        constexpr int RS = NT / CPR;                 // row groups
+        constexpr int TPC = NT / BN;                 // fold threads per column (first round)
+        static_assert(TPC >= 1 && RS * BN * 16 <= SMEM * 16, "GroupNorm partial staging");
+        const int cc = tid % CPR, rg = tid / CPR;
+        const bool colok = rg < RS && n0 + cc * 8 < a.N;
+        double2* red = (double2*)smem;
+        float x0[8], sm[8], sq[8];
+        int cnt = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { x0[e] = 0.f; sm[e] = 0.f; sq[e] = 0.f; }
+        auto acc = [&](const uint4& u) {
+          float f[8];
+          Vec16<T>::unpack(u, f);
+          if (cnt == 0) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x0[e] = f[e];
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float dv = f[e] - x0[e];
+            sm[e] += dv;
+            sq[e] = fmaf(dv, dv, sq[e]);
+          }
+          ++cnt;
+        };
+        if (colok) {
+          const int rend = min(BM, a.M - m0);
+          int row = rg;
+#pragma unroll 1
+          for (; row + RS < rend; row += 2 * RS) {
+            Src q0, q1;
+            fetch(row, cc, q0);
+            fetch(row + RS, cc, q1);
+            acc(combine(row, cc, q0));
+            acc(combine(row + RS, cc, q1));
+          }
+          if (row < rend) {
+            Src q0;
+            fetch(row, cc, q0);
+            acc(combine(row, cc, q0));
+          }
+        }
+        __syncthreads();        // every read of the staged tile is done before `red` overlays it
+        if (rg < RS) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const double x = x0[e], sd = sm[e];
+            red[rg * BN + cc * 8 + e] = make_double2(cnt * x + sd, cnt * x * x + 2.0 * x * sd + (double)sq[e]);
+          }
+        }
+        __syncthreads();
+        // round 1: TPC threads per column over row groups j, j + TPC, ...; round 2: the TPC sums in order
+        double2 v1 = make_double2(0.0, 0.0);
+        const int col1 = tid / TPC, j1 = tid % TPC;
+        if (col1 < BN)
+          for (int g = j1; g < RS; g += TPC) {
+            const double2 v = red[g * BN + col1];
+            v1.x += v.x;
+            v1.y += v.y;
+          }
+        __syncthreads();
+        if (col1 < BN) red[tid] = v1;
+        __syncthreads();
+        for (int col = tid; col < BN; col += NT) {
+          if (n0 + col >= a.N) continue;
+          double A = 0.0, B = 0.0;
+#pragma unroll
+          for (int j = 0; j < TPC; ++j) {
+            const double2 v = red[col * TPC + j];
+            A += v.x;
+            B += v.y;
+          }
+          *(double2*)(a.gn_part + ((long)(m0 / BM) * a.N + n0 + col) * 2) = make_double2(A, B);
+        }
+        return;
+      }
 #pragma unroll 1
       for (int idx = tid; idx < BM * CPR; idx += NT) {
         const int row = idx / CPR, c = idx - row * CPR;
@@ -798,6 +914,21 @@ bool gemm_gn_fusable(const GemmArgs& a) {
   return g_gn_fuse && g_large_tiles && is16(a.dtype) && eligible(a) && halo_bn(a) != 0;
 }
 
+int g_gn_parts = 1;
+
+int gemm_emits_gn_parts(const GemmArgs& a) {
+  if (!g_gn_parts || !g_large_tiles || !is16(a.dtype) || !eligible(a) || !vec_ok(a)) return 0;
+  if (a.geglu || a.hs_L || a.batch != 1 || a.out_f32) return 0;
+  if (halo_bn(a)) return a.M % 256 == 0 ? 256 : 0;
+  const Choice c = choose(a);
+  if (c.BM == 0 || a.M % c.BM) return 0;
+  if (c.splits > 1) {   // the in-kernel split-K reduction runs the epilogue; the separate reduce kernel does not
+    const long tiles = (long)((a.M + c.BM - 1) / c.BM) * ((a.N + c.BN - 1) / c.BN);
+    if (!(g_splitk_inkernel && c.splits == 2 && tiles <= kSplitCounters)) return 0;
+  }
+  return c.BM;
+}
+
 bool gemm_geglu_fusable(const GemmArgs& a) {
   if (!g_large_tiles || !a.geglu || !eligible(a) || !vec_ok(a)) return false;
   return choose(a).BM != 0;
@@ -835,6 +966,7 @@ int halo_bn(const GemmArgs& a) {
 bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   if (!eligible(a)) return false;
   IRX_CHECK(!a.gn_ab || halo_bn(a), "GroupNorm-fused operand needs the halo conv path");
+  IRX_CHECK(!a.gn_part || gemm_emits_gn_parts(a), "GroupNorm partials need the large-tile epilogue");
   if (const int hbn = halo_bn(a)) {
     GemmArgs b = a;
     b.vec_epilogue = 1;

@@ -114,7 +114,7 @@ static GemmArgs conv_args(int dt, const Act& x0, const Act* x1, const void* w, c
 }
 
 void Model::gn_conv3(Ctx& c, const Act& x0, const Act* x1, P g, P gb, float eps, int silu, P w, P b, int cout,
-                     const Act& out, const float* rowadd, long rowadd_ld, const void* residual) {
+                     Act& out, const float* rowadd, long rowadd_ld, const void* residual, bool stats) {
   const int C = x0.c + (x1 ? x1->c : 0);
   GemmArgs a = conv_args(dt_, x0, x1, ptr(w), b.set ? fptr(b) : nullptr, cout, 3, 1, 1, 1, x0.h, x0.w, out, rowadd,
                          rowadd_ld, residual, 0, -1);
@@ -127,25 +127,34 @@ void Model::gn_conv3(Ctx& c, const Act& x0, const Act* x1, P g, P gb, float eps,
     c.ws->free(ws);
     a.gn_ab = ab;
     a.gn_silu = silu;
-    run_gemm(c, a);
+    run_gemm(c, a, stats ? &out : nullptr);
     c.ws->free(ab);
     return;
   }
   Act n = new_act(c, x0.n, x0.h, x0.w, C);
   gnorm(c, x0, x1, g, gb, eps, silu, n);
-  conv2d(c, n, nullptr, w, b, cout, 3, 1, 1, 1, x0.h, x0.w, out, rowadd, rowadd_ld, residual);
+  conv2d(c, n, nullptr, w, b, cout, 3, 1, 1, 1, x0.h, x0.w, out, rowadd, rowadd_ld, residual, 0, -1, stats);
   drop(c, n);
 }
 
 void Model::conv2d(Ctx& c, const Act& x0, const Act* x1, P w, P b, int cout, int k, int stride, int pad_t,
-                   int pad_l, int hv, int wv, const Act& out, const float* rowadd, long rowadd_ld,
-                   const void* residual, int out_f32, int ldc) {
+                   int pad_l, int hv, int wv, Act& out, const float* rowadd, long rowadd_ld,
+                   const void* residual, int out_f32, int ldc, bool stats) {
   GemmArgs a = conv_args(dt_, x0, x1, ptr(w), b.set ? fptr(b) : nullptr, cout, k, stride, pad_t, pad_l, hv, wv, out,
                          rowadd, rowadd_ld, residual, out_f32, ldc);
-  run_gemm(c, a);
+  run_gemm(c, a, stats && ldc < 0 ? &out : nullptr);
 }
 
-void Model::run_gemm(Ctx& c, GemmArgs& a) {
+void Model::run_gemm(Ctx& c, GemmArgs& a, Act* stats) {
+  // GroupNorm partials of the output, kept with the activation until it is dropped (shape-only decision)
+  if (stats && !stats->gnp) {
+    const int r = gemm_emits_gn_parts(a);
+    if (r > 0 && (long)stats->h * stats->w % r == 0) {
+      stats->gnp = (double*)c.ws->alloc((size_t)(a.M / r) * a.N * 2 * sizeof(double));
+      stats->gnr = r;
+      a.gn_part = stats->gnp;
+    }
+  }
   const size_t ws = gemm_workspace_bytes(a);     // split-K partials (shape-only decision)
   void* p = ws ? c.ws->alloc(ws) : nullptr;
   if (!c.ws->dry()) {
@@ -157,7 +166,7 @@ void Model::run_gemm(Ctx& c, GemmArgs& a) {
 }
 
 void Model::linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, const float* bias, void* C, long ldc,
-                   int act, const void* residual, long ldr, int out_f32, int imgs) {
+                   int act, const void* residual, long ldr, int out_f32, int imgs, Act* stats) {
   GemmArgs a;
   a.dtype = dt_;
   a.M = M; a.N = N; a.K = K;
@@ -169,14 +178,21 @@ void Model::linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, co
   a.residual = residual; a.ldr = ldr;
   a.out_f32 = out_f32;
   a.imgs = imgs;
-  run_gemm(c, a);
+  run_gemm(c, a, stats && ldc == N ? stats : nullptr);
 }
 
 void Model::gnorm(Ctx& c, const Act& x0, const Act* x1, P g, P b, float eps, int silu, const Act& out) {
   void* ws = c.ws->alloc(gn_ws_bytes(x0.n, x0.h * x0.w, cfg_.norm_groups));
-  if (!c.ws->dry())
-    group_norm(dt_, x0.p, x1 ? x1->p : nullptr, x0.c, x1 ? x1->c : 0, x0.n, x0.h * x0.w, cfg_.norm_groups, eps,
-               fptr(g), fptr(b), silu, out.p, ws, c.s);
+  const bool parts = x0.gnp && (!x1 || x1->gnp);   // every source's producer emitted its partial sums
+  if (!c.ws->dry()) {
+    if (parts)
+      group_norm_parts(dt_, x0.p, x1 ? x1->p : nullptr, x0.c, x1 ? x1->c : 0, x0.n, x0.h * x0.w, cfg_.norm_groups,
+                       eps, fptr(g), fptr(b), silu, out.p, x0.gnp, x0.gnr, x1 ? x1->gnp : nullptr,
+                       x1 ? x1->gnr : 0, ws, c.s);
+    else
+      group_norm(dt_, x0.p, x1 ? x1->p : nullptr, x0.c, x1 ? x1->c : 0, x0.n, x0.h * x0.w, cfg_.norm_groups, eps,
+                 fptr(g), fptr(b), silu, out.p, ws, c.s);
+  }
   c.ws->free(ws);
 }
 
@@ -310,7 +326,7 @@ Act Unet::resnet(Ctx& c, const ResW& r, Act& x0, Act* x1, const float* tproj, fl
   IRX_CHECK(cin == r.cin, "resnet channel mismatch");
   Act h1 = new_act(c, B, H, W, r.cout);
   gn_conv3(c, x0, x1, r.n1w, r.n1b, eps, 1, r.c1w, r.c1b, r.cout, h1, tproj ? tproj + r.temb_off : nullptr,
-           temb_cols_);
+           temb_cols_, nullptr, true);
   Act sc;
   const void* res = x0.p;
   if (r.shortcut) {
@@ -319,7 +335,7 @@ Act Unet::resnet(Ctx& c, const ResW& r, Act& x0, Act* x1, const float* tproj, fl
     res = sc.p;
   }
   Act out = new_act(c, B, H, W, r.cout);
-  gn_conv3(c, h1, nullptr, r.n2w, r.n2b, eps, 1, r.c2w, r.c2b, r.cout, out, nullptr, 0, res);
+  gn_conv3(c, h1, nullptr, r.n2w, r.n2b, eps, 1, r.c2w, r.c2b, r.cout, out, nullptr, 0, res, true);
   drop(c, h1);
   if (r.shortcut) drop(c, sc);
   return out;
@@ -417,7 +433,7 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   c.ws->free(att);
   c.ws->free(n);
   Act out = new_act(c, B, x.h, x.w, C);
-  linear(c, h.p, C, M, C, a.pow, C, fptr(a.pob), out.p, C, ACT_NONE, x.p, C, 0, B);
+  linear(c, h.p, C, M, C, a.pow, C, fptr(a.pob), out.p, C, ACT_NONE, x.p, C, 0, B, &out);
   drop(c, h);
   return out;
 }
@@ -443,7 +459,7 @@ void Unet::run(Ctx& c, const void* x, int B, int h, int w, const float* t, const
   Act xin;
   xin.p = const_cast<void*>(x); xin.n = B; xin.h = h; xin.w = w; xin.c = cin_pad_;
   Act cur = new_act(c, B, h, w, bo[0]);
-  conv2d(c, xin, nullptr, conv_in_w, conv_in_b, bo[0], 3, 1, 1, 1, h, w, cur);
+  conv2d(c, xin, nullptr, conv_in_w, conv_in_b, bo[0], 3, 1, 1, 1, h, w, cur, nullptr, 0, nullptr, 0, -1, true);
   std::vector<Act> skips{cur};
   bool cur_is_skip = true;
   for (auto& blk : down_) {
@@ -462,7 +478,7 @@ void Unet::run(Ctx& c, const void* x, int B, int h, int w, const float* t, const
     if (blk.resample) {
       const int Ho = (cur.h - 1) / 2 + 1, Wo = (cur.w - 1) / 2 + 1;
       Act d = new_act(c, B, Ho, Wo, blk.ch);
-      conv2d(c, cur, nullptr, blk.rsw, blk.rsb, blk.ch, 3, 2, 1, 1, cur.h, cur.w, d);
+      conv2d(c, cur, nullptr, blk.rsw, blk.rsb, blk.ch, 3, 2, 1, 1, cur.h, cur.w, d, nullptr, 0, nullptr, 0, -1, true);
       skips.push_back(d);
       cur = d;
     }
@@ -492,7 +508,7 @@ void Unet::run(Ctx& c, const void* x, int B, int h, int w, const float* t, const
       // Upsample2D: nearest resize to the next skip's size (== 2x unless a latent side is not /8)
       const int th = skips.back().h, tw = skips.back().w;
       Act u = new_act(c, B, th, tw, blk.ch);
-      conv2d(c, cur, nullptr, blk.rsw, blk.rsb, blk.ch, 3, 1, 1, 1, th, tw, u);
+      conv2d(c, cur, nullptr, blk.rsw, blk.rsb, blk.ch, 3, 1, 1, 1, th, tw, u, nullptr, 0, nullptr, 0, -1, true);
       drop(c, cur);
       cur = u;
     }
@@ -613,7 +629,7 @@ Act Vae::resnet(Ctx& c, const ResW& r, Act& x) {
   const float eps = cfg_.norm_eps;
   const int B = x.n, H = x.h, W = x.w;
   Act h1 = new_act(c, B, H, W, r.cout);
-  gn_conv3(c, x, nullptr, r.n1w, r.n1b, eps, 1, r.c1w, r.c1b, r.cout, h1);
+  gn_conv3(c, x, nullptr, r.n1w, r.n1b, eps, 1, r.c1w, r.c1b, r.cout, h1, nullptr, 0, nullptr, true);
   Act sc;
   const void* res = x.p;
   if (r.shortcut) {
@@ -622,7 +638,7 @@ Act Vae::resnet(Ctx& c, const ResW& r, Act& x) {
     res = sc.p;
   }
   Act out = new_act(c, B, H, W, r.cout);
-  gn_conv3(c, h1, nullptr, r.n2w, r.n2b, eps, 1, r.c2w, r.c2b, r.cout, out, nullptr, 0, res);
+  gn_conv3(c, h1, nullptr, r.n2w, r.n2b, eps, 1, r.c2w, r.c2b, r.cout, out, nullptr, 0, res, true);
   drop(c, h1);
   if (r.shortcut) drop(c, sc);
   return out;
@@ -685,7 +701,7 @@ Act Vae::attn(Ctx& c, const AttW& a, Act& x) {
   c.ws->free(qkv);
   c.ws->free(VT);
   Act out = new_act(c, B, x.h, x.w, C);
-  linear(c, O, C, M, C, a.ow, C, fptr(a.ob), out.p, C, ACT_NONE, x.p, C, 0, B);
+  linear(c, O, C, M, C, a.ow, C, fptr(a.ob), out.p, C, ACT_NONE, x.p, C, 0, B, &out);
   c.ws->free(O);
   return out;
 }
@@ -696,7 +712,7 @@ void Vae::run_encode(Ctx& c, const void* img, int B, int H, int W, void* moments
   Act x;
   x.p = const_cast<void*>(img); x.n = B; x.h = H; x.w = W; x.c = 8;
   Act cur = new_act(c, B, H, W, bo[0]);
-  conv2d(c, x, nullptr, e_cin_w, e_cin_b, bo[0], 3, 1, 1, 1, H, W, cur);
+  conv2d(c, x, nullptr, e_cin_w, e_cin_b, bo[0], 3, 1, 1, 1, H, W, cur, nullptr, 0, nullptr, 0, -1, true);
   for (int i = 0; i < nb; ++i) {
     for (auto& r : e_res_[i]) {
       Act nx = resnet(c, r, cur);
@@ -707,7 +723,8 @@ void Vae::run_encode(Ctx& c, const void* img, int B, int H, int W, void* moments
       // Downsample2D(padding=0): F.pad(x, (0,1,0,1)) then 3x3 stride-2 conv
       const int Ho = (cur.h + 1 - 3) / 2 + 1, Wo = (cur.w + 1 - 3) / 2 + 1;
       Act d = new_act(c, B, Ho, Wo, cur.c);
-      conv2d(c, cur, nullptr, e_down_w_[i], e_down_b_[i], cur.c, 3, 2, 0, 0, cur.h, cur.w, d);
+      conv2d(c, cur, nullptr, e_down_w_[i], e_down_b_[i], cur.c, 3, 2, 0, 0, cur.h, cur.w, d, nullptr, 0, nullptr, 0, -1,
+             true);
       drop(c, cur);
       cur = d;
     }
@@ -735,7 +752,7 @@ void Vae::run_decode(Ctx& c, const void* z, int B, int h, int w, void* out) {
   Act zq = new_act(c, B, h, w, 8);
   linear(c, z, 8, (long)B * h * w, 8, pqw, 8, fptr(pqb), zq.p, 8, ACT_NONE, nullptr, 0, 0, B);
   Act cur = new_act(c, B, h, w, cm);
-  conv2d(c, zq, nullptr, d_cin_w, d_cin_b, cm, 3, 1, 1, 1, h, w, cur);
+  conv2d(c, zq, nullptr, d_cin_w, d_cin_b, cm, 3, 1, 1, 1, h, w, cur, nullptr, 0, nullptr, 0, -1, true);
   drop(c, zq);
   Act r = resnet(c, d_mid0_, cur);
   drop(c, cur);
@@ -751,7 +768,8 @@ void Vae::run_decode(Ctx& c, const void* z, int B, int h, int w, void* out) {
     }
     if (i < nb - 1) {
       Act u = new_act(c, B, cur.h * 2, cur.w * 2, cur.c);
-      conv2d(c, cur, nullptr, d_up_w_[i], d_up_b_[i], cur.c, 3, 1, 1, 1, cur.h * 2, cur.w * 2, u);
+      conv2d(c, cur, nullptr, d_up_w_[i], d_up_b_[i], cur.c, 3, 1, 1, 1, cur.h * 2, cur.w * 2, u, nullptr, 0, nullptr, 0,
+             -1, true);
       drop(c, cur);
       cur = u;
     }

@@ -44,6 +44,8 @@ struct ParamEntry {
 struct Act {   // NHWC activation view
   void* p = nullptr;
   int n = 0, h = 0, w = 0, c = 0;
+  double* gnp = nullptr;   // GroupNorm partials emitted by its producer (GemmArgs::gn_part), else null
+  int gnr = 0;             // ... rows per partial (divides h * w)
   long pix() const { return (long)n * h * w; }
 };
 
@@ -71,18 +73,27 @@ class Model {
   // ---- op helpers (skip launches in dry-run mode)
   struct Ctx { hipStream_t s; Arena* ws; };
   Act new_act(Ctx& c, int n, int h, int w, int ch);
-  void drop(Ctx& c, Act& a) { c.ws->free(a.p); a.p = nullptr; }
+  void drop(Ctx& c, Act& a) {
+    c.ws->free(a.p);
+    a.p = nullptr;
+    if (a.gnp) c.ws->free(a.gnp);
+    a.gnp = nullptr;
+    a.gnr = 0;
+  }
+  // `stats`: the output feeds a GroupNorm -> the epilogue also emits its partial sums when it can (Act::gnp)
   void conv2d(Ctx& c, const Act& x0, const Act* x1, P w, P b, int cout, int k, int stride, int pad_t, int pad_l,
-              int hv, int wv, const Act& out, const float* rowadd = nullptr, long rowadd_ld = 0,
-              const void* residual = nullptr, int out_f32 = 0, int ldc = -1);
+              int hv, int wv, Act& out, const float* rowadd = nullptr, long rowadd_ld = 0,
+              const void* residual = nullptr, int out_f32 = 0, int ldc = -1, bool stats = false);
   void linear(Ctx& c, const void* A, long lda, int M, int K, P w, int N, const float* bias, void* C, long ldc,
-              int act = ACT_NONE, const void* residual = nullptr, long ldr = 0, int out_f32 = 0, int imgs = 0);
-  void run_gemm(Ctx& c, GemmArgs& a);   // allocates split-K partials from the workspace when needed
+              int act = ACT_NONE, const void* residual = nullptr, long ldr = 0, int out_f32 = 0, int imgs = 0,
+              Act* stats = nullptr);
+  void run_gemm(Ctx& c, GemmArgs& a, Act* stats = nullptr);   // split-K partials / GroupNorm partials
   void gnorm(Ctx& c, const Act& x0, const Act* x1, P g, P b, float eps, int silu, const Act& out);
   // GroupNorm(+SiLU) of (x0 | x1) followed by a 3x3 / stride-1 / pad-1 conv into `out`: folded into the
   // conv's halo operand path where it fits (gemm_gn_fusable), else a normalised copy and the plain conv
   void gn_conv3(Ctx& c, const Act& x0, const Act* x1, P g, P gb, float eps, int silu, P w, P b, int cout,
-                const Act& out, const float* rowadd = nullptr, long rowadd_ld = 0, const void* residual = nullptr);
+                Act& out, const float* rowadd = nullptr, long rowadd_ld = 0, const void* residual = nullptr,
+                bool stats = false);
   void lnorm(Ctx& c, const void* x, int rows, int C, P g, P b, float eps, void* out);
 
   int kind_;

@@ -211,6 +211,57 @@ __global__ __launch_bounds__(256) void gn_finalize3_kernel(const double* __restr
   }
 }
 
+// GroupNorm from producer partials (GemmArgs::gn_part): per (image, group of 8 GroupNorm groups) block, 32
+// threads per group fold the image's row-block partials of the group's channels (x0 then x1, fixed order)
+// in fp64 -> (mean, rstd) -> the channels' scale / shift.  Replaces the statistics pass over the tensor.
+__global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const double2* __restrict__ p0, int C0, int rpi0,
+                                                                const double2* __restrict__ p1, int C1, int rpi1,
+                                                                int G, double cnt, float eps,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta,
+                                                                float2* __restrict__ ab) {
+  __shared__ float2 gmr[8];
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int C = C0 + C1, cg = C / G;
+  const int gl = t >> 5, sub = t & 31, g = blockIdx.y * 8 + gl;
+  double a = 0.0, b = 0.0;
+  if (g < G) {
+    // the group's channels [g*cg, g*cg + cg) split at the concat seam: c0s channels from x0, the rest from x1
+    const int cb = g * cg, c0s = max(0, min(cg, C0 - cb));
+    const int tot0 = rpi0 * c0s, tot1 = rpi1 * (cg - c0s);
+#pragma unroll 4
+    for (int i = sub; i < tot0; i += 32) {
+      const int r = i / c0s, ch = cb + (i - r * c0s);
+      const double2 v = p0[((long)n * rpi0 + r) * C0 + ch];
+      a += v.x;
+      b += v.y;
+    }
+    const int c1b = cb + c0s - C0, c1s = cg - c0s;
+#pragma unroll 4
+    for (int i = sub; i < tot1; i += 32) {
+      const int r = i / c1s, ch = c1b + (i - r * c1s);
+      const double2 v = p1[((long)n * rpi1 + r) * C1 + ch];
+      a += v.x;
+      b += v.y;
+    }
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
+  if (sub == 0 && g < G) {
+    const double mean = a / cnt;
+    double var = b / cnt - mean * mean;
+    if (var < 0.0) var = 0.0;
+    gmr[gl] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+  }
+  __syncthreads();
+  const int c0 = blockIdx.y * 8 * cg, c1 = min(C, c0 + 8 * cg);
+  for (int c = c0 + t; c < c1; c += 256) {
+    const float2 r = gmr[(c - c0) / cg];
+    const float sc = r.y * gamma[c];
+    ab[(long)n * C + c] = make_float2(sc, fmaf(-r.x, sc, beta[c]));
+  }
+}
+
 // per-channel scale / shift from (mean, rstd) (after the v1 finalize)
 __global__ __launch_bounds__(256) void gn_ab_kernel(const float2* __restrict__ mr, int G, int C,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -383,9 +434,20 @@ float2* gn_ab_ws(void* ws, int N, int G) {
 
 template <typename T>
 void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps, const float* gamma,
-          const float* beta, int silu, void* out, void* ws, hipStream_t s) {
+          const float* beta, int silu, void* out, void* ws, hipStream_t s, const double* p0 = nullptr, int r0 = 0,
+          const double* p1 = nullptr, int r1 = 0) {
   float2* ab = gn_ab_ws(ws, N, G);
-  gn_stats_t<T>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, ab, ws, s);
+  if (p0) {
+    ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_finalize_parts_kernel") : std::string(),
+                 0.0, s);
+    gn_finalize_parts_kernel<<<dim3(N, (G + 7) / 8), 256, 0, s>>>((const double2*)p0, C0, HW / r0,
+                                                                  (const double2*)p1, C1, r1 ? HW / r1 : 0, G,
+                                                                  (double)HW * ((C0 + C1) / G), eps, gamma, beta,
+                                                                  ab);
+    IRX_LAUNCH_CHECK();
+  } else {
+    gn_stats_t<T>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, ab, ws, s);
+  }
   const int C = C0 + C1;
   const int VEC = 16 / (int)sizeof(T);
   // ~16 pixels per thread per block, one fixed channel chunk per thread
@@ -447,6 +509,19 @@ void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N
   if (dtype == F32) gn_t<float>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s);
   else if (dtype == F16) gn_t<f16_t>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s);
   else gn_t<bf16_t>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s);
+}
+
+void group_norm_parts(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
+                      const float* gamma, const float* beta, int silu, void* out, const double* p0, int r0,
+                      const double* p1, int r1, void* ws, hipStream_t s) {
+  const int vec = dtype == F32 ? 4 : 8;
+  IRX_CHECK(G > 0 && G <= 64 && (C0 + C1) % G == 0, "GroupNorm: C must divide into <= 64 groups");
+  IRX_CHECK(C0 % vec == 0 && C1 % vec == 0 && C0 + C1 <= kMaxC, "GroupNorm: channel counts");
+  IRX_CHECK(p0 && r0 > 0 && HW % r0 == 0 && (C1 == 0 || (x1 && p1 && r1 > 0 && HW % r1 == 0)),
+            "GroupNorm partials missing");
+  if (dtype == F32) gn_t<float>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s, p0, r0, p1, r1);
+  else if (dtype == F16) gn_t<f16_t>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s, p0, r0, p1, r1);
+  else gn_t<bf16_t>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, silu, out, ws, s, p0, r0, p1, r1);
 }
 
 void group_norm_stats(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,

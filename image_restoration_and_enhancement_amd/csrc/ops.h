@@ -50,6 +50,10 @@ struct GemmArgs {
   // channel c of image n becomes gn_act(x, gn_ab[n][c].x, gn_ab[n][c].y, gn_silu); c indexes the C0 + C1
   // concat.  Zero padding stays zero (it pads the normalised tensor, as in the unfused form).
   const float2* gn_ab = nullptr; int gn_silu = 0;
+  // GroupNorm statistics of the OUTPUT emitted by the epilogue: per block of R output rows (R = the tile's BM,
+  // gemm_emits_gn_parts) and per output channel, the (sum, sum of squares) of the stored values as double2 at
+  // gn_part[(m / R) * N + n] (shifted fp32 sums per thread, fp64 merge: gn_stats3's arithmetic)
+  double* gn_part = nullptr;
   void* splitk_ws = nullptr; size_t splitk_ws_bytes = 0;   // caller workspace for split-K partials
   int dbg = 0;            // large-tile diagnostics (irx_set_option("gemm_dbg")): 1 skip epilogue, 2 skip MFMAs
 };
@@ -68,6 +72,8 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path
 size_t gemm_workspace_bytes(const GemmArgs& a);           // split-K partial buffer the call will use
 bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can apply the GEGLU epilogue
 bool gemm_gn_fusable(const GemmArgs& a);                  // conv can apply GemmArgs::gn_ab to its operand
+int gemm_emits_gn_parts(const GemmArgs& a);   // rows per GroupNorm partial this call's epilogue emits (0: none)
+extern int g_gn_parts;     // 1: producers emit GroupNorm partial sums, the stats pass is skipped (0: A/B)
 extern int g_gn_fuse;      // 1: GroupNorm(+SiLU) folded into the following halo conv where it fits (0: A/B)
 extern bool g_large_tiles;
 extern int g_gemm_deep;    // large-tile pipeline: 0 two-stage BK 64, 1 BK-32 S-stage ring, 2 BK-64 deeper ring
@@ -86,6 +92,11 @@ extern int g_conv_halo;      // 3x3 convs on whole-row tiles: one LDS halo per 3
 extern bool g_gn_v2;       // GroupNorm stats v3 (slabbed grid + finalize kernel); 0 = v1 (A/B)
 void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
                 const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s);
+// GroupNorm from producer partials (GemmArgs::gn_part of x0 / x1, r0 / r1 rows each, dividing HW): finalize +
+// apply, no statistics pass over the tensor
+void group_norm_parts(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
+                      const float* gamma, const float* beta, int silu, void* out, const double* p0, int r0,
+                      const double* p1, int r1, void* ws, hipStream_t s);
 // statistics only: per (image, channel) scale / shift (gamma * rstd, beta - mean * gamma * rstd) into
 // `ab` [N][C0 + C1] (float2), for a consumer that applies them itself (GemmArgs::gn_ab)
 void group_norm_stats(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,

@@ -29,6 +29,8 @@ CONVS = [  # (label, N, H, W, C0, C1, Cout, k, stride, up)
 ]
 GEMMS = [  # (label, M, N, K)
     ("lin320x320@64", 65536, 320, 320),
+    ("lin640x640@32", 16384, 640, 640),
+    ("lin1280@16b", 4096, 1280, 1280),
     ("qkv@64", 65536, 960, 320),
     ("ff1@64", 65536, 2560, 320),
     ("ff2@64", 65536, 320, 1280),
@@ -71,7 +73,7 @@ def main():
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
     base = {"large_tiles": 1, "gemm_deep": 0, "gemm_small": 0, "tile_256x320": 1, "splitk_inkernel": 1}
-    allv = {"s2": {}, "ring64": {"gemm_deep": 2}, "small": {"gemm_small": 1}, "4wave": {"large_tiles": 0},
+    allv = {"s2": {}, "ring64": {"gemm_deep": 2}, "ring32": {"gemm_deep": 1}, "small": {"gemm_small": 1}, "4wave": {"large_tiles": 0},
             "no320": {"tile_256x320": 0}, "redk": {"splitk_inkernel": 0}, "no320redk": {"tile_256x320": 0, "splitk_inkernel": 0}}
     variants = [(v, allv[v]) for v in args.variants.split(",")]
 
