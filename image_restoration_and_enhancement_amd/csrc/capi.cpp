@@ -66,6 +66,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gn_v2") g_gn_v2 = value != 0;
   else if (n == "gn_fuse") g_gn_fuse = value;
   else if (n == "gn_parts") g_gn_parts = value;
+  else if (n == "halo_split") g_halo_split = value;
   else if (n == "vae_attn_rows") g_vae_attn_rows = value;
   else if (n == "splitk_inkernel") g_splitk_inkernel = value != 0;
   else if (n == "tile_256x320") g_tile_256x320 = value != 0;

@@ -315,19 +315,20 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         hb[i] = Vec16<T>::pack(f);
       }
     };
-    const int nk = kt1;   // (kt0 == 0)
-    issueH(0);
+    // this split's K steps [kt0, nk): whole slabs (host: sp.per is a multiple of 9)
+    const int nk = kt1, c0 = kt0 / 9;
+    issueH(c0);
 #pragma unroll
     for (int p = 0; p < S - 1; ++p)
-      if (p < nk) issueB(p, p);
+      if (kt0 + p < nk) issueB(kt0 + p, p);
     __syncthreads();      // zero row visible
     if (gab) {
-      wait_vm(IPB * min(S - 1, nk));                     // this wave's halo-0 pieces landed (B pieces may fly)
+      wait_vm(IPB * min(S - 1, nk - kt0));               // this wave's first-halo pieces landed (B pieces may fly)
       __syncthreads();
-      transformH(0, 0, 9 - S);                           // visible after the first main-loop barrier
+      transformH(c0, 0, 9 - S);                          // visible after the first main-loop barrier
     }
     int st = 0;
-    for (int kt = 0; kt < nk; ++kt) {
+    for (int kt = kt0; kt < nk; ++kt) {
       const int c = kt / 9, t = kt - 9 * c;
       // younger than B(kt): B(kt+1 .. kt+S-2), and slab c+1's halo while it was issued after B(kt)
       int allow = IPB * min(S - 2, nk - 1 - kt);
@@ -524,8 +525,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         }
         return;
       }
-      // one 16-byte output chunk: its operands (staged tile, residual, row add) fetched first, then the final
-      // value (row add, residual, output scale) formed and stored — split so two rows' loads overlap
+      // one 16-byte output chunk: its operands (staged tile, residual, row add), then the final value (row add,
+      // residual, output scale) formed and stored
       struct Src { uint4 u, r; float4 x, y; };
       auto fetch = [&](int row, int c, Src& q) {
         const int m = m0 + row, n = n0 + c * 8;
@@ -591,16 +592,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         };
         if (colok) {
           const int rend = min(BM, a.M - m0);
-          int row = rg;
+          // (one row per step: a two-row software pipeline here pushed the 128x128 tiles past 128 VGPRs,
+          //  i.e. from two resident blocks per CU to one)
 #pragma unroll 1
-          for (; row + RS < rend; row += 2 * RS) {
-            Src q0, q1;
-            fetch(row, cc, q0);
-            fetch(row + RS, cc, q1);
-            acc(combine(row, cc, q0));
-            acc(combine(row + RS, cc, q1));
-          }
-          if (row < rend) {
+          for (int row = rg; row < rend; row += RS) {
             Src q0;
             fetch(row, cc, q0);
             acc(combine(row, cc, q0));
@@ -936,16 +931,34 @@ bool gemm_geglu_fusable(const GemmArgs& a) {
 
 int halo_bn(const GemmArgs& a);
 
+int halo_splits(const GemmArgs& a, long tiles);
+
 size_t gemm_workspace_bytes(const GemmArgs& a) {
-  if (!g_large_tiles || !eligible(a) || halo_bn(a)) return 0;
+  if (!g_large_tiles || !eligible(a)) return 0;
+  if (halo_bn(a)) {
+    const int sp = halo_splits(a, canon_rows(a) / 256 * (a.N / 160));
+    return sp > 1 ? (size_t)sp * a.M * a.N * sizeof(float) : 0;
+  }
   const Choice c = choose(a);
   if (c.BM == 0 || c.splits <= 1) return 0;
   return (size_t)c.splits * a.batch * ((a.M + c.BM - 1) / c.BM * c.BM) * ((a.N + c.BN - 1) / c.BN * c.BN) *
          sizeof(float);
 }
 
+// K splits of a halo conv (whole 64-channel slabs per split): 1 when the tiles fill the chip, 2 (in-kernel
+// reduction) when two splits do, 0 = the halo path does not take the shape.
+int g_halo_split = 1;   // irx_set_option("halo_split", 0): no K-split halo tiles (A/B)
+
+int halo_splits(const GemmArgs& a, long tiles) {
+  if (tiles >= kCUs || g_conv_halo >= 2) return 1;
+  if (!g_halo_split) return 0;
+  const int slabs = (a.g.C0 + a.g.C1) / 64;
+  if (g_splitk_inkernel && 2 * tiles >= kCUs && slabs >= 8 && tiles <= kSplitCounters) return 2;
+  return 0;
+}
+
 // Halo tile (BN) for a 3x3 / stride-1 / pad-1 conv whose 256-pixel tiles are whole image rows and whose
-// grid fills the chip; 0 = not applicable.
+// grid fills the chip (alone or with two K splits); 0 = not applicable.
 int halo_bn(const GemmArgs& a) {
   const ConvGeom& g = a.g;
   if (!g_conv_halo || !a.conv || a.batch != 1 || a.geglu || a.out_f32 || !vec_ok(a)) return 0;
@@ -956,7 +969,7 @@ int halo_bn(const GemmArgs& a) {
   if (W < 16 || W > kHaloWMax || (W & (W - 1)) || 256 % W || g.Hin % (256 / W)) return 0;
   if ((long)g.N * g.Hin * W != a.M || a.M % 256) return 0;
   const int bn = a.N % 160 == 0 ? 160 : 0;
-  if (!bn || (g_conv_halo < 2 && canon_rows(a) / 256 * (a.N / bn) < kCUs)) return 0;
+  if (!bn || !halo_splits(a, canon_rows(a) / 256 * (a.N / bn))) return 0;
   // (GroupNorm-fused operand: one 512-element chunk of the (256 + 2W) x 8 halo per tap, taps 3..8)
   static_assert((256 + 2 * kHaloWMax) * 8 <= 512 * 6, "halo normalisation chunks");
   return bn;
@@ -973,6 +986,18 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     b.dbg = g_gemm_dbg;
     Split sp;
     sp.per = a.K / 64;
+    const int splits = halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));
+    if (splits > 1) {   // whole slabs per split, in-kernel last-arriver reduction (fp32 partials)
+      const int slabs = (a.g.C0 + a.g.C1) / 64;
+      sp.splits = splits;
+      sp.per = 9 * ((slabs + splits - 1) / splits);
+      sp.Mp = a.M;
+      sp.Np = a.N;
+      const size_t need = (size_t)splits * a.M * a.N * sizeof(float);
+      sp.ws = (a.splitk_ws && a.splitk_ws_bytes >= need) ? (float*)a.splitk_ws : internal_ws(need);
+      sp.inkernel = true;
+      sp.cnt = stream_counters(s);
+    }
     launch2<256, 160, 4, 2, 64, 3, true>(b, sp, s);
     return true;
   }

@@ -354,8 +354,8 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   drop(c, gn);
   void* n = c.ws->alloc(M * C * es);
   void* att = c.ws->alloc(M * C * es);
-  // self-attention
   lnorm(c, h.p, M, C, a.ln1w, a.ln1b, 1e-5f, n);
+  // self-attention
   void* qkv = c.ws->alloc(M * 3 * C * es);
   // 16-bit engines: q|k|v written head-major ([q|k|v][image][head][token][d], GemmArgs::hs_*) so each attention
   // block streams its head's K / V rows contiguously
@@ -387,8 +387,8 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   }
   c.ws->free(qkv);
   linear(c, att, C, M, C, a.o1w, C, fptr(a.o1b), h.p, C, ACT_NONE, h.p, C, 0, B);
-  // cross-attention (K|V precomputed per prompt)
   lnorm(c, h.p, M, C, a.ln2w, a.ln2b, 1e-5f, n);
+  // cross-attention (K|V precomputed per prompt)
   {
     GemmArgs g;
     g.dtype = dt_; g.M = M; g.N = C; g.K = C;
@@ -409,8 +409,8 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     attention(aa, c.s);
   }
   linear(c, n, C, M, C, a.o2w, C, fptr(a.o2b), h.p, C, ACT_NONE, h.p, C, 0, B);
-  // GEGLU feed-forward: fused into the projection's epilogue when the large-tile path takes the shape
   lnorm(c, h.p, M, C, a.ln3w, a.ln3b, 1e-5f, n);
+  // GEGLU feed-forward: fused into the projection's epilogue when the large-tile path takes the shape
   void* g = c.ws->alloc(M * 4 * C * es);
   {
     GemmArgs ga;

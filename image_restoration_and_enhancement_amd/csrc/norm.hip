@@ -374,7 +374,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long l
       const int v = lane + 64 * i;
       if (v < nv) {
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) { const float dd = f[i][e] - mean; q += dd * dd; }
+        for (int e = 0; e < VEC; ++e) { const float dd = f[i][e] - mean; q = fmaf(dd, dd, q); }
       }
     }
 #pragma unroll
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long l
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
           const int c = v * VEC + e;
-          y[e] = (f[i][e] - mean) * rstd * gamma[c] + beta[c];
+          y[e] = fmaf((f[i][e] - mean) * rstd, gamma[c], beta[c]);   // (the form the fused epilogue shares)
         }
         *(uint4*)(out + (long)row * ldo + v * VEC) = Vec16<T>::pack(y);
       }

@@ -202,3 +202,30 @@ def test_vae_attention_row_blocks_bit_exact(device, denoise_sd, dtype):
             L.call("irx_set_option", b"vae_attn_rows", 0)
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("opt,dtype", [("gn_parts", "bf16"), ("gn_parts", "fp16")])
+def test_unet_gn_parts_close_to_stats_pass(device, denoise_sd, opt, dtype):
+    """The GroupNorm partials from the producer epilogues (`gn_parts`) change only the statistics' summation
+    order: the UNet output stays within 1e-2 relative L2 of the stats-pass form."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    pc, sd = denoise_sd
+    unet = UNet(pc.unet, dtype, device)
+    unet.load_state_dict(sd["unet"])
+    B, h, w = 2, 32, 32
+    g = torch.Generator().manual_seed(3)
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float16
+    xin = torch.zeros(B, h, w, unet.cin_pad)
+    xin[..., :4] = torch.randn(B, h, w, 4, generator=g)
+    ctx = torch.randn(B, 77, 768, generator=g)
+    kv = unet.prepare_context(ctx.to(tdt).to(device).contiguous())
+    x = xin.to(tdt).to(device).contiguous()
+    t = torch.full((B,), 601.0, device=device)
+    outs = []
+    for v in (1, 0):
+        L.call("irx_set_option", opt.encode(), v)
+        try:
+            outs.append(unet.forward(x, t, kv, 77).clone())
+        finally:
+            L.call("irx_set_option", opt.encode(), 1)
+    assert rel_l2(outs[0].cpu(), outs[1].cpu()) < 1e-2

@@ -366,6 +366,7 @@ def test_conv_halo(device, halo_forced, case, dt):
     (2, 64, 64, 320, 0, 320, False, False),
     (1, 64, 64, 640, 320, 320, True, False),   # up-block concat (groups of 30 straddle the seam) + temb + residual
     (1, 32, 32, 1280, 640, 640, True, False),
+    (2, 16, 16, 1280, 0, 1280, True, False),   # 16x16 level: two K splits
     (2, 16, 32, 128, 64, 160, True, True),
     (1, 16, 16, 64, 64, 160, False, True),
 ])
@@ -414,11 +415,11 @@ def test_gn_conv3_fused_bit_exact(device, case, dt, silu):
 
 
 def test_gn_conv3_not_fusable_is_refused(device):
-    """Shapes off the halo path (16x16 level at batch 2, odd widths) report fused = 0 and the launch fails loudly
-    (the models fall back to a normalised copy + plain conv)."""
+    """Shapes off the halo path (the 8x8 level: rows narrower than 16 pixels) report fused = 0 and the launch
+    fails loudly (the models fall back to a normalised copy + plain conv)."""
     from image_restoration_and_enhancement_amd import _lib as L
     dt = torch.bfloat16
-    x = _dev(_r(2, 16, 16, 1280, seed=98), dt, device)
+    x = _dev(_r(2, 8, 8, 1280, seed=98), dt, device)
     g = torch.ones(1280, device=device)
     w = _r(1280, 1280, 3, 3, seed=99, scale=0.01)
     L.call("irx_set_option", b"gn_fuse", 1)
@@ -428,6 +429,36 @@ def test_gn_conv3_not_fusable_is_refused(device):
             O.gn_conv3(x, g, g, 1e-5, w, None)
     finally:
         L.call("irx_set_option", b"gn_fuse", 0)
+
+
+@pytest.mark.parametrize("case", [
+    # (N, H, W, C0, C1, Cout, rowadd+residual): the UNet's 16x16-level convs, whose 128 halo tiles take two
+    # K splits (whole 64-channel slabs, in-kernel reduction)
+    (2, 16, 16, 1280, 0, 1280, True),
+    (1, 16, 16, 1280, 1280, 1280, True),   # up-block concat
+    (3, 16, 16, 640, 0, 1280, False),      # down2 resnet 0 conv1 (10 slabs)
+])
+@pytest.mark.parametrize("dt", DT16)
+def test_conv_halo_split_k(device, case, dt):
+    N, H, W, C0, C1, Co, extra = case
+    x0 = _r(N, C0, H, W, seed=180)
+    x1 = _r(N, C1, H, W, seed=181) if C1 else None
+    w = _r(Co, C0 + C1, 3, 3, seed=182, scale=1 / math.sqrt((C0 + C1) * 9))
+    b = _r(Co, seed=183)
+    temb = _r(N, Co, seed=184) if extra else None
+    res = _r(N, H, W, Co, seed=185) if extra else None
+    got = O.conv2d(_dev(x0.permute(0, 2, 3, 1), dt, device), w.to(dt).float(), b,
+                   x1=_dev(x1.permute(0, 2, 3, 1), dt, device) if C1 else None,
+                   rowadd=temb.to(device).contiguous() if extra else None,
+                   residual=_dev(res, dt, device) if extra else None)
+    xin = torch.cat([_q(x0, dt)] + ([_q(x1, dt)] if C1 else []), 1)
+    ref = F.conv2d(xin, _q(w, dt), b, padding=1)
+    if extra:
+        ref = ref + temb[:, :, None, None]
+    ref = ref.permute(0, 2, 3, 1)
+    if extra:
+        ref = ref + _q(res, dt)
+    assert O.rel_err(got, ref) < TOL[dt]
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
