@@ -84,7 +84,6 @@ class SDEngine:
         # HIP-graph replay of repeated denoising loops (IRX_GRAPHS=0 disables)
         self.use_graphs = os.environ.get("IRX_GRAPHS", "1") != "0" and self.device.type == "cuda"
         self._graphs: Dict[tuple, dict] = {}
-        self._graph_seen: set = set()
         self._graph_stream = torch.cuda.Stream(self.device) if self.use_graphs else None
 
     def __del__(self):
@@ -166,9 +165,10 @@ class SDEngine:
     def denoise_loop(self, lat: torch.Tensor, kv: torch.Tensor, plans: List[StepPlan], guidance: float,
                      cfg_on: bool, mask_l: Optional[torch.Tensor] = None,
                      masked_l: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """The denoising loop.  With `use_graphs`, the second call of an identical loop (shapes, plans, guidance)
-        records it as one HIP graph (irx_graph_*) on the engine's stream and every later call replays it into
-        persistent buffers: ~600 launches per UNet eval issued by one hipGraphLaunch."""
+        """The denoising loop.  With `use_graphs`, the first call of a loop (shapes, plans, guidance) runs eagerly
+        on the engine's stream and then records the same loop as one HIP graph (irx_graph_*) into persistent
+        buffers — host-only work that overlaps the eager kernels still queued on the GPU; every later call
+        replays it: ~600 launches per UNet eval issued by one hipGraphLaunch."""
         if not self.use_graphs or not lat.is_cuda:
             return self._loop_body(lat, kv, plans, guidance, cfg_on, mask_l, masked_l,
                                    self._loop_buffers(lat, plans, cfg_on))
@@ -180,14 +180,13 @@ class SDEngine:
         gs.wait_stream(cs)
         with torch.cuda.stream(gs):
             g = self._graphs.get(key)
-            if g is None and key not in self._graph_seen:
-                # first sight: eager on the graph stream (sizes the workspaces, creates its split-K tickets)
-                self._graph_seen.add(key)
+            if g is None:
+                # first sight: eager on the graph stream (sizes the workspaces, creates its split-K tickets), then
+                # record the graph for the next call while those kernels run
                 out = self._loop_body(lat, kv, plans, guidance, cfg_on, mask_l, masked_l,
                                       self._loop_buffers(lat, plans, cfg_on))
+                self._capture(key, lat, kv, plans, guidance, cfg_on, mask_l, masked_l)
             else:
-                if g is None:
-                    g = self._capture(key, lat, kv, plans, guidance, cfg_on, mask_l, masked_l)
                 g["lat"].copy_(lat)
                 g["kv"].copy_(kv)
                 if mask_l is not None:

@@ -28,7 +28,7 @@ def test_graph_replay_equals_eager(device, dtype, kind, res, batch):
     imgs = torch.from_numpy(np.stack([MC.smooth_image(res, res, seed=70 + i) for i in range(batch)])).to(device)
     eager = _engine(device, dtype, False, kind=kind).img2img(imgs, prompt, strength, 20, guidance, seed=42)
     eng = _engine(device, dtype, True, kind=kind)
-    outs = [eng.img2img(imgs, prompt, strength, 20, guidance, seed=42) for _ in range(3)]   # eager, capture, replay
+    outs = [eng.img2img(imgs, prompt, strength, 20, guidance, seed=42) for _ in range(3)]   # eager + capture, replays
     assert len(eng._graphs) == 1
     for o in outs:
         assert torch.equal(o.latents, eager.latents)
