@@ -783,6 +783,154 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// attnw: flash attention for wide heads (the VAE mid-block's single d = 512 head), bf16 / fp16, non-causal.
+// Block = 4 waves x the same 32 queries; wave w owns d-quarter w.  Per 32-key tile:
+//   partial S^T_w = K[:, d_w] Q[:, d_w]^T (D/64 k-steps of v_mfma_f32_32x32x16, K fragments straight from
+//   global: every K element is read by exactly one wave of the block) -> LDS -> every wave sums the four
+//   partials in the same order (identical S^T in all waves) -> online softmax in base 2 (scale * log2 e at the
+//   Q load; fp32 running max / row sum) -> P^T as the B operand of O^T_w += V^T P^T over the wave's D/4
+//   rows (V tile staged once per block in LDS, V^T fragments by ds_read_tr16_b64).  Scores never leave LDS.
+template <typename T, int D, int QG>
+__global__ __launch_bounds__(256, QG == 1 ? 2 : 1) void attnw_kernel(AttnArgs a) {
+  // QG query groups of 32 per block; the 4 / QG waves of a group split d (DW each)
+  constexpr int KT = 32, WPG = 4 / QG, DW = D / WPG, NSW = DW / 16, NDTW = DW / 32;
+  constexpr int SV = (D % 128 == 32 || D % 128 == 96) ? D : D + 32;   // ds_read_tr rows conflict-free
+  constexpr int VCH = D / 8;                                           // 16-byte chunks per V row
+  static_assert(D % 128 == 0 && (KT * VCH) % 256 == 0, "attnw shape");
+  __shared__ float Sx[4][64 * 16];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[KT * SV];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5, g = lane >> 4;
+  const int nq = (a.Lq + 32 * QG - 1) / (32 * QG);
+  const int qb = blockIdx.x % nq, bh = blockIdx.x / nq;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int qg = wave / WPG, dw = wave - qg * WPG;
+  const int qrow = (qb * QG + qg) * 32 + r;
+  const T* __restrict__ Q = (const T*)a.q + (long)b * a.sq + (long)h * (a.hsq ? a.hsq : D);
+  const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : D);
+  const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : D);
+  const int d0 = dw * DW;
+
+  uint4 qf[NSW];
+  const float sl2 = a.scale * 1.4426950408889634f;
+#pragma unroll
+  for (int s = 0; s < NSW; ++s) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (qrow < a.Lq) v = *(const uint4*)(Q + (long)qrow * a.ldq + d0 + 16 * s + 8 * hh);
+    if (!a.q_scaled) {
+      float f[8];
+      Vec16<T>::unpack(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= sl2;
+      v = Vec16<T>::pack(f);
+    }
+    qf[s] = v;
+  }
+  f32x16 oacc[NDTW];
+#pragma unroll
+  for (int i = 0; i < NDTW; ++i)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) oacc[i][k] = 0.f;
+  float m = -INFINITY, lsum = 0.f;
+
+  for (int j0 = 0; j0 < a.Lk; j0 += KT) {
+    // K fragments of this wave's d-quarter: lane (r, hh) = key j0 + r, d0 + 16 s + 8 hh .. +7
+    const int key = j0 + r;
+    f32x16 sp;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sp[k] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NSW; ++s) {
+      const uint4 kf = key < a.Lk ? *(const uint4*)(K + (long)key * a.ldk + d0 + 16 * s + 8 * hh) : make_uint4(0, 0, 0, 0);
+      sp = Mfma<T>::m32x32x16(kf, qf[s], sp);
+    }
+    __syncthreads();   // the previous tile's Sx / Vs reads are done
+#pragma unroll
+    for (int k = 0; k < 16; ++k) Sx[wave][k * 64 + lane] = sp[k];
+#pragma unroll
+    for (int u = 0; u < KT * VCH / 256; ++u) {
+      const int idx = tid + 256 * u, row = idx / VCH, c = idx - row * VCH;
+      const int kk = j0 + row;
+      *(uint4*)(Vs + row * SV + c * 8) =
+          kk < a.Lk ? *(const uint4*)(V + (long)kk * a.ldv + c * 8) : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    f32x16 sacc;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      float v = Sx[qg * WPG][k * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < WPG; ++w) v += Sx[qg * WPG + w][k * 64 + lane];
+      const int kk = j0 + (k & 3) + 8 * (k >> 2) + 4 * hh;
+      sacc[k] = kk < a.Lk ? v : -INFINITY;
+    }
+    float tmax = sacc[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) tmax = fmaxf(tmax, sacc[k]);
+    tmax = fmaxf(tmax, xlane32(tmax));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m - mn);
+    m = mn;
+    lsum *= alpha;
+#pragma unroll
+    for (int i = 0; i < NDTW; ++i)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) oacc[i][k] *= alpha;
+    uint4 pb[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float p[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        p[j] = __builtin_amdgcn_exp2f(sacc[8 * s2 + j] - mn);
+        lsum += p[j];
+      }
+      pb[s2] = make_uint4(Mfma<T>::pack2(p[0], p[1]), Mfma<T>::pack2(p[2], p[3]), Mfma<T>::pack2(p[4], p[5]),
+                          Mfma<T>::pack2(p[6], p[7]));
+    }
+#pragma unroll
+    for (int dt = 0; dt < NDTW; ++dt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int krow = 16 * s2 + 4 * (g >> 1) + ((lane & 15) >> 2);
+        const int col = d0 + 32 * dt + 16 * (g & 1) + 4 * (lane & 3);
+        const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + krow * SV + col));
+        const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + (krow + 8) * SV + col));
+        const uint4 vf = make_uint4(__builtin_bit_cast(uint2, t1).x, __builtin_bit_cast(uint2, t1).y,
+                                    __builtin_bit_cast(uint2, t2).x, __builtin_bit_cast(uint2, t2).y);
+        oacc[dt] = Mfma<T>::m32x32x16(vf, pb[s2], oacc[dt]);
+      }
+  }
+  const float l = lsum + xlane32(lsum);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (qrow >= a.Lq) return;
+  T* __restrict__ O = (T*)a.o + (long)b * a.so + (long)h * (a.hso ? a.hso : D) + (long)qrow * a.ldo;
+#pragma unroll
+  for (int dt = 0; dt < NDTW; ++dt)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = d0 + 32 * dt + 8 * k + 4 * hh;
+      *(uint2*)(O + e) = make_uint2(Mfma<T>::pack2(oacc[dt][4 * k] * inv, oacc[dt][4 * k + 1] * inv),
+                                    Mfma<T>::pack2(oacc[dt][4 * k + 2] * inv, oacc[dt][4 * k + 3] * inv));
+    }
+}
+
+template <typename T>
+void launchw(const AttnArgs& a, hipStream_t s) {
+  const int qg = g_attnw_qg == 1 ? 1 : 2;
+  dim3 grid(((a.Lq + 32 * qg - 1) / (32 * qg)) * a.H * a.B), block(256);
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attnw_kernel<") +
+                               (std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short") + ", 512, " +
+                               std::to_string(qg) + ">"
+                         : std::string(),
+               4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
+  if (qg == 1) attnw_kernel<T, 512, 1><<<grid, block, 0, s>>>(a);
+  else attnw_kernel<T, 512, 2><<<grid, block, 0, s>>>(a);
+  IRX_LAUNCH_CHECK();
+}
+
 template <typename T, int D, int KT, bool CAUSAL>
 void launch3_cfg(const AttnArgs& a, hipStream_t s) {
   const int nq = (a.Lq + 127) / 128;
@@ -872,6 +1020,12 @@ void attention(const AttnArgs& a, hipStream_t s) {
   IRX_CHECK(((uintptr_t)a.k % 16) == 0 && ((uintptr_t)a.v % 16) == 0, "K/V base alignment");
   const bool v16 = a.d % 8 == 0 && (a.ldq % 8) == 0 && ((uintptr_t)a.q % 16) == 0 && ((uintptr_t)a.o % 8) == 0 &&
                    (a.ldo % 4) == 0;
+  if (a.d == 512 && a.dtype != F32) {
+    IRX_CHECK(!a.causal && v16 && (a.ldk % 8) == 0 && (a.ldv % 8) == 0, "d = 512 attention: 16-byte rows, non-causal");
+    if (a.dtype == F16) launchw<f16_t>(a, s);
+    else launchw<bf16_t>(a, s);
+    return;
+  }
   if (a.dtype == F32) launch_t<float>(a, s);
   else if (a.dtype == F16) {
     IRX_CHECK(v16 && launch3<f16_t>(a, s), "fp16 attention: head dim must be 40 / 64 / 80 / 160 with 16-byte rows");
@@ -880,6 +1034,7 @@ void attention(const AttnArgs& a, hipStream_t s) {
   else launch_t<bf16_t>(a, s);
 }
 int g_attn_v3 = 1;
+int g_attnw_qg = 1;   // irx_set_option("attnw_qg", 1|2): query groups of 32 per d = 512 flash block (2: measured slower)
 int g_attn_xcd = 1;
 int g_attn_hm = 1;
 

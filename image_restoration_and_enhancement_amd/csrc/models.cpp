@@ -644,14 +644,16 @@ Act Vae::resnet(Ctx& c, const ResW& r, Act& x) {
   return out;
 }
 
-// Mid-block single-head attention (d = 512), row-blocked: V transposed once, then per block of query rows
+// Mid-block single-head attention (d = 512).  16-bit engines: one flash launch (attnw_kernel).  fp32 (the
+// parity engine) and option vae_flash = 0: row-blocked, V transposed once, then per block of query rows
 // (all images batched) fp32 scores S = Q K^T * C^-1/2 -> row softmax -> P V, with the score block capped
 // at kVaeScoreBytes whatever the resolution (8 x 9216^2 fp32 scores at 768^2 would be 2.7 GB).  Every row
 // is computed exactly as in one block (K-ordered MFMA sums, no split-K at K = 512 / HWp), so the result does
 // not depend on the blocking.  The key axis is padded to a multiple of 8 (zero probabilities / zero V^T
 // columns) so the PV contraction stays 16-byte aligned.
 constexpr size_t kVaeScoreBytes = 128u << 20;
-int g_vae_attn_rows = 0;   // irx_set_option("vae_attn_rows", R): force R query rows per block (tests); 0 = auto
+int g_vae_attn_rows = 0;
+int g_vae_flash = 1;       // irx_set_option("vae_flash", 0): the row-blocked GEMM form in the 16-bit engines too   // irx_set_option("vae_attn_rows", R): force R query rows per block (tests); 0 = auto
 
 Act Vae::attn(Ctx& c, const AttW& a, Act& x) {
   const int B = x.n, HW = x.h * x.w, C = a.c;
@@ -663,6 +665,25 @@ Act Vae::attn(Ctx& c, const AttW& a, Act& x) {
   void* qkv = c.ws->alloc(M * 3 * C * es);
   linear(c, gn.p, C, M, C, a.qkvw, 3 * C, fptr(a.qkvb), qkv, 3 * C, ACT_NONE, nullptr, 0, 0, B);
   drop(c, gn);
+  if (dt_ != F32 && C == 512 && g_vae_flash) {
+    // 16-bit engines: one flash-attention launch (attnw_kernel), no score memory at all
+    void* O = c.ws->alloc(M * C * es);
+    if (!c.ws->dry()) {
+      AttnArgs aa;
+      aa.dtype = dt_; aa.B = B; aa.H = 1; aa.Lq = HW; aa.Lk = HW; aa.d = C;
+      aa.scale = 1.0f / std::sqrt((float)C);
+      aa.q = qkv; aa.ldq = 3 * C; aa.sq = (long)HW * 3 * C;
+      aa.k = (char*)qkv + C * es; aa.ldk = 3 * C; aa.sk = aa.sq;
+      aa.v = (char*)qkv + 2 * C * es; aa.ldv = 3 * C; aa.sv = aa.sq;
+      aa.o = O; aa.ldo = C; aa.so = (long)HW * C;
+      attention(aa, c.s);
+    }
+    c.ws->free(qkv);
+    Act out = new_act(c, B, x.h, x.w, C);
+    linear(c, O, C, M, C, a.ow, C, fptr(a.ob), out.p, C, ACT_NONE, x.p, C, 0, B, &out);
+    c.ws->free(O);
+    return out;
+  }
   void* VT = c.ws->alloc((size_t)B * C * HWp * es);
   if (!c.ws->dry()) {
     if (HWp != HW) IRX_HIP(hipMemsetAsync(VT, 0, (size_t)B * C * HWp * es, c.s));

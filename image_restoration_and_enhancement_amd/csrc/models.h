@@ -10,6 +10,7 @@
 namespace irx {
 
 extern int g_vae_attn_rows;   // VAE mid-block attention: query rows per score block (0 = auto, capped bytes)
+extern int g_vae_flash;       // VAE mid-block attention in the 16-bit engines: flash kernel (1) / row-blocked (0)
 
 // Deterministic first-fit allocator over a caller-owned workspace.  Run once with base == nullptr
 // ("dry run": no kernels launched) to size the workspace, then for real with identical calls.

@@ -194,12 +194,14 @@ def test_vae_attention_row_blocks_bit_exact(device, denoise_sd, dtype):
     z = torch.randn(2, 32, 32, 8, generator=g)
     x, z = x.to(tdt).to(device).contiguous(), z.to(tdt).to(device).contiguous()
     outs = []
-    for rows in (0, 256):
-        L.call("irx_set_option", b"vae_attn_rows", rows)
-        try:
+    L.call("irx_set_option", b"vae_flash", 0)        # (the 16-bit engines otherwise take the flash kernel)
+    try:
+        for rows in (0, 256):
+            L.call("irx_set_option", b"vae_attn_rows", rows)
             outs.append((vae.encode(x).clone(), vae.decode(z).clone()))
-        finally:
-            L.call("irx_set_option", b"vae_attn_rows", 0)
+    finally:
+        L.call("irx_set_option", b"vae_attn_rows", 0)
+        L.call("irx_set_option", b"vae_flash", 1)
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
 
@@ -229,3 +231,30 @@ def test_unet_gn_parts_close_to_stats_pass(device, denoise_sd, opt, dtype):
         finally:
             L.call("irx_set_option", opt.encode(), 1)
     assert rel_l2(outs[0].cpu(), outs[1].cpu()) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_vae_flash_attention_vs_row_blocked(device, denoise_sd, dtype):
+    """16-bit VAE with the d = 512 flash kernel vs the row-blocked GEMM form of the mid-block attention: the
+    encoder agrees to relative L2 < 1e-2; the decoder, whose later layers amplify the attention's rounding
+    differences, to < 5e-2 (the bf16 decoder's bound against the fp32 oracle, test_fullsize_gpu.py)."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    from image_restoration_and_enhancement_amd.engine import VAE, TORCH_DT, dtype_code
+    pc, sd = denoise_sd
+    tdt = TORCH_DT[dtype_code(dtype)]
+    vae = VAE(pc.vae, dtype, device)
+    vae.load_state_dict(sd["vae"])
+    g = torch.Generator().manual_seed(6)
+    x = (torch.rand(2, 128, 128, 8, generator=g) * 2 - 1)
+    x[..., 3:] = 0
+    z = torch.randn(2, 24, 40, 8, generator=g)
+    x, z = x.to(tdt).to(device).contiguous(), z.to(tdt).to(device).contiguous()
+    outs = []
+    for flash in (1, 0):
+        L.call("irx_set_option", b"vae_flash", flash)
+        try:
+            outs.append((vae.encode(x).float().cpu(), vae.decode(z).float().cpu()))
+        finally:
+            L.call("irx_set_option", b"vae_flash", 1)
+    assert rel_l2(outs[0][0], outs[1][0]) < 1e-2
+    assert rel_l2(outs[0][1], outs[1][1]) < 5e-2
