@@ -835,27 +835,38 @@ __global__ __launch_bounds__(256, QG == 1 ? 2 : 1) void attnw_kernel(AttnArgs a)
     for (int k = 0; k < 16; ++k) oacc[i][k] = 0.f;
   float m = -INFINITY, lsum = 0.f;
 
+  // K fragments (lane (r, hh) = key j0 + r, d0 + 16 s + 8 hh .. +7) and this thread's V-tile chunks are
+  // register-prefetched one tile ahead, so their latency hides under the previous tile's softmax and PV MFMAs
+  constexpr int NVU = KT * VCH / 256;
+  uint4 kn[NSW], vn[NVU];
+  auto fetch = [&](int j) {
+    const int key = j + r;
+#pragma unroll
+    for (int s = 0; s < NSW; ++s)
+      kn[s] = key < a.Lk ? *(const uint4*)(K + (long)key * a.ldk + d0 + 16 * s + 8 * hh) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < NVU; ++u) {
+      const int idx = tid + 256 * u, row = idx / VCH, c = idx - row * VCH;
+      const int kk = j + row;
+      vn[u] = kk < a.Lk ? *(const uint4*)(V + (long)kk * a.ldv + c * 8) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  fetch(0);
   for (int j0 = 0; j0 < a.Lk; j0 += KT) {
-    // K fragments of this wave's d-quarter: lane (r, hh) = key j0 + r, d0 + 16 s + 8 hh .. +7
-    const int key = j0 + r;
     f32x16 sp;
 #pragma unroll
     for (int k = 0; k < 16; ++k) sp[k] = 0.f;
 #pragma unroll
-    for (int s = 0; s < NSW; ++s) {
-      const uint4 kf = key < a.Lk ? *(const uint4*)(K + (long)key * a.ldk + d0 + 16 * s + 8 * hh) : make_uint4(0, 0, 0, 0);
-      sp = Mfma<T>::m32x32x16(kf, qf[s], sp);
-    }
+    for (int s = 0; s < NSW; ++s) sp = Mfma<T>::m32x32x16(kn[s], qf[s], sp);
     __syncthreads();   // the previous tile's Sx / Vs reads are done
 #pragma unroll
     for (int k = 0; k < 16; ++k) Sx[wave][k * 64 + lane] = sp[k];
 #pragma unroll
-    for (int u = 0; u < KT * VCH / 256; ++u) {
+    for (int u = 0; u < NVU; ++u) {
       const int idx = tid + 256 * u, row = idx / VCH, c = idx - row * VCH;
-      const int kk = j0 + row;
-      *(uint4*)(Vs + row * SV + c * 8) =
-          kk < a.Lk ? *(const uint4*)(V + (long)kk * a.ldv + c * 8) : make_uint4(0, 0, 0, 0);
+      *(uint4*)(Vs + row * SV + c * 8) = vn[u];
     }
+    if (j0 + KT < a.Lk) fetch(j0 + KT);   // registers free again: the next tile's loads fly under this softmax / PV
     __syncthreads();
     f32x16 sacc;
 #pragma unroll
@@ -917,17 +928,16 @@ __global__ __launch_bounds__(256, QG == 1 ? 2 : 1) void attnw_kernel(AttnArgs a)
     }
 }
 
+// (QG = 2 query groups per block was measured slower — one wave per SIMD — and spills with the prefetch: only
+//  QG = 1 is instantiated)
 template <typename T>
 void launchw(const AttnArgs& a, hipStream_t s) {
-  const int qg = g_attnw_qg == 1 ? 1 : 2;
-  dim3 grid(((a.Lq + 32 * qg - 1) / (32 * qg)) * a.H * a.B), block(256);
+  dim3 grid(((a.Lq + 31) / 32) * a.H * a.B), block(256);
   ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attnw_kernel<") +
-                               (std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short") + ", 512, " +
-                               std::to_string(qg) + ">"
+                               (std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short") + ", 512, 1>"
                          : std::string(),
                4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
-  if (qg == 1) attnw_kernel<T, 512, 1><<<grid, block, 0, s>>>(a);
-  else attnw_kernel<T, 512, 2><<<grid, block, 0, s>>>(a);
+  attnw_kernel<T, 512, 1><<<grid, block, 0, s>>>(a);
   IRX_LAUNCH_CHECK();
 }
 
@@ -1034,7 +1044,6 @@ void attention(const AttnArgs& a, hipStream_t s) {
   else launch_t<bf16_t>(a, s);
 }
 int g_attn_v3 = 1;
-int g_attnw_qg = 1;   // irx_set_option("attnw_qg", 1|2): query groups of 32 per d = 512 flash block (2: measured slower)
 int g_attn_xcd = 1;
 int g_attn_hm = 1;
 

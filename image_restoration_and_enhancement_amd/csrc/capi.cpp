@@ -69,7 +69,6 @@ int irx_set_option(const char* name, int value) {
   else if (n == "halo_split") g_halo_split = value;
   else if (n == "vae_attn_rows") g_vae_attn_rows = value;
   else if (n == "vae_flash") g_vae_flash = value;
-  else if (n == "attnw_qg") g_attnw_qg = value;
   else if (n == "splitk_inkernel") g_splitk_inkernel = value != 0;
   else if (n == "tile_256x320") g_tile_256x320 = value != 0;
   else if (n == "gemm_force") g_gemm_force = value;

@@ -128,7 +128,6 @@ extern bool g_attn_v2;
 extern int g_attn_v3;    // 32x32x16 kernel for bf16 / fp16 (0: the round-1 kernels, bf16 only)
 extern int g_attn_xcd;   // 1: (batch, head) groups of q-blocks kept on one XCD (K/V shared in its L2)
 extern int g_attn_hm;    // 1: the UNet's q|k|v projections write head-major attention operands
-extern int g_attnw_qg;   // d = 512 flash kernel: query groups of 32 per block (1 or 2)
 extern int g_attn_d40;   // bf16: 16x16x32 kernel (irx_set_option("attn_v2", 0) selects the 16x16x16 one)
 
 // ------------------------------------------------------------ elementwise / data movement
