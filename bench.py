@@ -135,10 +135,11 @@ def build_engine(cfg, dtype, device, rank):
         blobs = {k: m.pack(sds[k]).to(device) for k, m in models.items()}
     else:
         blobs = {k: torch.empty(m.blob_bytes(), dtype=torch.uint8, device=device) for k, m in models.items()}
-    D.broadcast_blobs(blobs)            # RCCL broadcast of the frozen weights over xGMI (N > 1)
     for k, m in models.items():
         m.bind_blob(blobs[k])
-    return eng, sds
+    # RCCL broadcast of the frozen weights over xGMI (N > 1): irx_weights_bcast through the C ABI
+    how = D.broadcast_models(models)
+    return eng, sds, how
 
 
 def pmc_traffic(kernel: str):
@@ -204,7 +205,8 @@ def cpu_baseline_and_parity(eng_bf16, sds, device, n_images: int, threads: int) 
            "sample": f"BASELINE configs[0]: {n_images} full 512x512 denoise image(s), 20 PNDM steps x strength 0.5 "
                      f"= {len(refs[0].timesteps)} UNet evals with CFG 5.0 (batch 2), VAE encode + decode, fp32 "
                      f"PyTorch-CPU restatement (oracle/pipeline_ref.py), torch threads = usable CPUs of this "
-                     f"process ({threads}); {per_img:.1f} s/image, model load excluded"}
+                     f"process ({threads}); {per_img:.1f} s/image, model load excluded",
+           "seconds_per_image": [round(t, 2) for t in t_img]}
 
     # the same images through the GPU engine
     u8 = torch.from_numpy(noisy).to(device).contiguous()
@@ -234,6 +236,8 @@ def cpu_baseline_and_parity(eng_bf16, sds, device, n_images: int, threads: int) 
               "images": n_images,
               "fp32_engine_max_abs_vs_ref": f32_max, "fp32_engine_u8_max_diff_vs_ref": u8_max,
               "psnr_vs_ref": round(float(np.mean(ps)), 3), "ssim_vs_ref": round(float(np.mean(ss)), 5),
+              "psnr_vs_ref_per_image": [round(float(x), 3) for x in ps],
+              "ssim_vs_ref_per_image": [round(float(x), 5) for x in ss],
               "psnr_gt": {"gpu_bf16": round(float(np.mean(ps_gt_g)), 4), "cpu_ref": round(float(np.mean(ps_gt_c)), 4)},
               "ssim_gt": {"gpu_bf16": round(float(np.mean(ss_gt_g)), 5), "cpu_ref": round(float(np.mean(ss_gt_c)), 5)},
               "note": "psnr/ssim_vs_ref: GPU bf16 output against the CPU fp32 reference output (metrics.py = "
@@ -251,7 +255,7 @@ def main():
     ap.add_argument("--sched-steps", type=int, default=50)
     ap.add_argument("--dtype", default=None, help="bf16 | fp16 | fp32 (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-images", type=int, default=1, help="configs[0] images for the CPU baseline")
+    ap.add_argument("--cpu-images", type=int, default=4, help="configs[0] images for the CPU baseline (configs[0]: 4)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--opt", action="append", default=[], help="irx_set_option name=value (A/B experiments)")
     args = ap.parse_args()
@@ -273,7 +277,7 @@ def main():
     cfg = PipelineConfig.default(args.task)
     cfg.scheduler.kind = "ddim"          # BASELINE.json: "50 DDIM steps" (explicit override of the saved PNDM)
     t_init = time.perf_counter()
-    eng, sds = build_engine(cfg, dtype, device, rank)
+    eng, sds, bcast = build_engine(cfg, dtype, device, rank)
     u8_h, mask_h = task_inputs(args.task, spec, batch, seed=rank)
     imgs = torch.from_numpy(u8_h).to(device).contiguous()
     mask = torch.from_numpy(mask_h).to(device).contiguous() if mask_h is not None else None
@@ -356,7 +360,8 @@ def main():
                                                  if cfg_f == 2 else "no CFG")
                                    + (", 9-channel UNet, 2 VAE encodes" if args.task == "inpaint" else ""),
                        "task": args.task, "global_batch": batch * world, "resolution": res,
-                       "parallelism": f"dp{world}", "tflop_per_image": round(tflop_img, 2),
+                       "parallelism": f"dp{world}", "weights_bcast": bcast,
+                       "tflop_per_image": round(tflop_img, 2),
                        "achieved_tflops_end_to_end": round(value * tflop_img, 1), "outputs_finite": finite},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
         }

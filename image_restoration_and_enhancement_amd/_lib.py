@@ -110,7 +110,14 @@ _SIGS = {
     "irx_op_gemm": (i32, [vp, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, f32, i32, vp, i64, i32, i32, i64,
                           i64, i64, i64]),
     "irx_op_group_norm": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, vp]),
+    "irx_rccl_available": (i32, []),
+    "irx_rccl_unique_id": (i32, [C.c_char_p]),
+    "irx_rccl_comm_init": (i32, [C.c_char_p, i32, i32, C.POINTER(vp)]),
+    "irx_rccl_comm_destroy": (i32, [vp]),
+    "irx_rccl_broadcast": (i32, [vp, vp, sz, i32, vp]),
+    "irx_weights_bcast": (i32, [vp, vp, i32, vp]),
     "irx_op_group_norm_ws_bytes": (sz, [i32, i32, i32]),
+    "irx_op_gn_conv3_ws_bytes": (sz, [i32, i32, i32, i32]),
     "irx_op_gn_conv3": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp, i64,
                               vp, vp, vp, vp]),
     "irx_op_layer_norm": (i32, [vp, i32, vp, i32, i32, f32, vp, vp, vp]),
@@ -147,7 +154,7 @@ def load(path: Path | str | None = None, force: bool = False):
 def call(name: str, *args):
     lib = load()
     rc = getattr(lib, name)(*args)
-    if _SIGS[name][0] is i32 and name not in ("irx_version",) and rc != 0:
+    if _SIGS[name][0] is i32 and name not in ("irx_version", "irx_rccl_available") and rc != 0:
         raise IrxError(f"{name}: {lib.irx_last_error().decode(errors='replace')}")
     return rc
 

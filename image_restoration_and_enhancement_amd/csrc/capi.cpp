@@ -67,6 +67,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gn_fuse") g_gn_fuse = value;
   else if (n == "gn_parts") g_gn_parts = value;
   else if (n == "halo_split") g_halo_split = value;
+  else if (n == "halo_pipe") g_halo_pipe = value;
   else if (n == "vae_attn_rows") g_vae_attn_rows = value;
   else if (n == "vae_flash") g_vae_flash = value;
   else if (n == "splitk_inkernel") g_splitk_inkernel = value != 0;
@@ -210,6 +211,14 @@ int irx_model_bind(irx_model* m, void* blob, size_t bytes) {
   IRX_API_BEGIN
   IRX_CHECK(m, "null model");
   m->m->bind(blob, bytes);
+  IRX_API_END
+}
+
+int irx_weights_bcast(irx_model* m, void* comm, int root, void* s) {
+  IRX_API_BEGIN
+  IRX_CHECK(m && m->m, "null model");
+  IRX_CHECK(m->m->blob(), "no weight blob bound (irx_model_bind first)");
+  rccl_broadcast(comm, m->m->blob(), m->m->blob_bytes(), root, S(s));
   IRX_API_END
 }
 
@@ -523,6 +532,12 @@ int irx_op_group_norm(void* s, int dtype, const void* x0, const void* x1, int c0
   IRX_API_END
 }
 size_t irx_op_group_norm_ws_bytes(int n, int hw, int groups) { return gn_ws_bytes(n, hw, groups); }
+static size_t gn_conv3_ab_bytes(int n, int channels) {
+  return ((size_t)n * channels * sizeof(float2) + 255) / 256 * 256;
+}
+size_t irx_op_gn_conv3_ws_bytes(int n, int hw, int groups, int channels) {
+  return gn_conv3_ab_bytes(n, channels) + gn_ws_bytes(n, hw, groups);
+}
 
 int irx_op_gn_conv3(void* s, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int h, int w,
                     int groups, float eps, const float* gamma, const float* beta, int silu, const void* weight,
@@ -548,7 +563,7 @@ int irx_op_gn_conv3(void* s, int dtype, const void* x0, const void* x1, int c0, 
   IRX_CHECK(*fused, "shape does not take the GroupNorm-fused conv path");
   IRX_CHECK(x0 && gamma && beta && weight && ws, "null buffer");
   float2* ab = (float2*)ws;
-  void* gws = (char*)ws + (((size_t)n * (c0 + c1) * sizeof(float2) + 255) / 256 * 256);
+  void* gws = (char*)ws + gn_conv3_ab_bytes(n, c0 + c1);
   group_norm_stats(dtype, x0, x1, c0, c1, n, h * w, groups, eps, gamma, beta, ab, gws, S(s));
   a.gn_ab = ab;
   a.gn_silu = silu;

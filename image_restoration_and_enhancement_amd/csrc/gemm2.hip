@@ -19,6 +19,7 @@
 #include <cmath>
 #include <map>
 #include <mutex>
+#include <type_traits>
 
 #include "ops.h"
 #include "profile.h"
@@ -78,7 +79,7 @@ __device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds_addr) {
 constexpr int kHaloWMax = 64;    // widest image row a halo tile takes (LDS: 2 x (BM + 2W) x 2BK B)
 
 template <typename T, int BM, int BN, int WM, int WN, int BK, int S, bool CONV, bool OUTF32, bool RESIZE,
-          bool HALO = false>
+          int HALO = 0>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kernel(GemmArgs a, Split sp) {
   constexpr int NW = WM * WN, NT = NW * 64;   // 8 waves (1 block/CU) or 4 waves (2 blocks/CU)
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
@@ -236,7 +237,134 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     }
   };
 
-  if constexpr (HALO) {
+  if constexpr (HALO == 2) {
+    // ---- software-pipelined halo main loop (the default halo path; no GroupNorm-fused operand).  A K step
+    //      (slab c = kt / 9, tap t = kt % 9) is two 32-deep sub-steps; the fragments of sub-step 1 are read
+    //      while sub-step 0's MFMAs run, and those of the NEXT step's sub-step 0 right after the barrier, under
+    //      sub-step 1's MFMAs: no wave ever waits on an LDS read at the head of a step (the form above requests
+    //      all of a step's fragments after the barrier and then stalls on them while all 8 waves flood the LDS).
+    //      B ring of S = 3 stages, two steps ahead: before the barrier of step kt every wave drains its reads
+    //      (lgkmcnt(0)), so after it the DMA of step kt+3 may overwrite step kt's stage.  Halo buffers: slab
+    //      c+2's halo is issued after the barrier of slab c's last tap (when every read of slab c's buffer has
+    //      returned) and has nine steps to land.  Every wave issues IPB B pieces and HPW halo pieces per issue
+    //      (surplus ones land in a scratch KiB), so one counted vmcnt per step covers both streams.
+    static_assert(S == 3 && KSUB == 2, "pipelined halo: 3-stage B ring, BK 64");
+    const int W = a.g.Win, H = a.g.Hin, lw = __builtin_ctz(W);
+    const int HW = H * W;
+    const int img = m0 / HW, y0 = (m0 - img * HW) >> lw;
+    const int nhi = (((BM >> lw) + 2) << lw) / RPI;   // halo wave-instructions (RPI pixel rows each)
+    constexpr int HPW = (BM + 2 * kHaloWMax) / RPI / NW;
+    static_assert(HPW * RPI * NW == BM + 2 * kHaloWMax, "uniform halo pieces per wave");
+    uint4* const Hb = smem;                           // [2][HB_U4]
+    uint4* const Bsm = smem + 2 * HB_U4;              // [S][BN * CPR]
+    uint4* const zrow = Bsm + S * BN * CPR;           // one zero pixel row: taps left / right of the image
+    uint4* const scratch = zrow + CPR;                // 1 KiB target of the surplus pieces
+    if (tid < CPR) zrow[tid] = uint4{0u, 0u, 0u, 0u};
+    auto swz = [](int r) { return CPR == 8 ? (r & 7) : (((r >> 2) & 1) << 1); };
+    constexpr int NBI = BN / RPI, IPB = (NBI + NW - 1) / NW;
+    const uint16_t* bro[IPB];
+#pragma unroll
+    for (int j = 0; j < IPB; ++j) {
+      const int q = wave * IPB + j, r = RPI * q + lane / CPR;
+      bro[j] = (q < NBI && n0 + r < a.N) ? Bp + (long)(n0 + r) * a.ldb + (((lane % CPR) ^ swz(r)) * 8) : nullptr;
+    }
+    auto issueB = [&](int kt, int st) {
+      const int c = kt / 9, t = kt - 9 * c;
+      const int off = t * Cin + c * BK;
+#pragma unroll
+      for (int j = 0; j < IPB; ++j) {
+        const int q = wave * IPB + j;
+        uint4* dst = q < NBI ? Bsm + st * BN * CPR + q * 64 : scratch;
+        glds16_asm(bro[j] ? bro[j] + off : zp, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
+      }
+    };
+    auto issueH = [&](int c) {
+      const bool second = c * BK >= a.g.C0;
+      const uint16_t* sb = second ? (const uint16_t*)a.g.src1 : (const uint16_t*)a.g.src0;
+      const int cs = second ? a.g.C1 : a.g.C0;
+      const int ch = second ? c * BK - a.g.C0 : c * BK;
+#pragma unroll
+      for (int j = 0; j < HPW; ++j) {
+        const int q = wave * HPW + j;
+        const int p = RPI * q + lane / CPR;
+        const int y = y0 - 1 + (p >> lw), x = p & (W - 1);
+        const bool ok = q < nhi && y >= 0 && y < H;
+        const uint16_t* src = ok ? sb + ((long)(img * H + y) * W + x) * cs + ch + (((lane % CPR) ^ swz(p)) * 8) : zp;
+        uint4* dst = q < nhi ? Hb + (c & 1) * HB_U4 + q * 64 : scratch;
+        glds16_asm(src, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
+      }
+    };
+    uint4 fa[KSUB][TM], fb[KSUB][TN];
+    // fragments of sub-step SS of K step kt (B stage st)
+    auto readF = [&](auto ss_c, int kt, int st) {
+      constexpr int SS = decltype(ss_c)::value;
+      const int c = kt / 9, t = kt - 9 * c;
+      const int ky = t / 3, kx = t - 3 * ky;
+      const int shift = ky * W + kx - 1;
+      const uint4* Hs = Hb + (c & 1) * HB_U4;
+      const uint4* Bs = Bsm + st * BN * CPR;
+      const int ck = SS * 4 + fgrp;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * TM * 16 + i * 16 + frow;
+        const int rx = r & (W - 1);
+        const int hp = r + shift;
+        const bool zero = (kx == 0 && rx == 0) || (kx == 2 && rx == W - 1);
+        fa[SS][i] = zero ? zrow[ck] : Hs[hp * CPR + (ck ^ swz(hp))];
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * TN * 16 + j * 16 + frow;
+        fb[SS][j] = Bs[r * CPR + (ck ^ swz(r))];
+      }
+    };
+    auto mma = [&](auto ss_c) {
+      constexpr int SS = decltype(ss_c)::value;
+      if (a.dbg & 2) return;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[SS][i], fb[SS][j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    // this split's K steps [kt0, nk): whole slabs (host: sp.per is a multiple of 9); >= 9 steps per split
+    const int nk = kt1, c0 = kt0 / 9, cend = (kt1 + 8) / 9;
+    const bool h1 = c0 + 1 < cend;
+    // halo issued "at step i" (after B(i + 3)): the prologue's H(c0 + 1) counts as step kt0 - 1
+    auto hasH = [&](int i) {
+      return i == kt0 - 1 ? h1 : (i >= kt0 && i - 9 * (i / 9) == 8 && i / 9 + 2 < cend);
+    };
+    issueH(c0);
+#pragma unroll
+    for (int p = 0; p < S; ++p) issueB(kt0 + p, p);
+    if (h1) issueH(c0 + 1);
+    wait_vm(2 * IPB + (h1 ? HPW : 0));                  // H(c0) and B(kt0) landed
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // (+ the zero row)
+    readF(S0{}, kt0, 0);
+    int st = 0;
+    for (int kt = kt0; kt < nk; ++kt) {
+      readF(S1{}, kt, st);
+      mma(S0{});
+      if (kt + 1 < nk) {
+        // younger than B(kt+1): B(kt+2), and a halo issued at step kt-1 or kt-2
+        const int allow = (kt + 2 < nk ? IPB : 0) + ((hasH(kt - 1) || hasH(kt - 2)) ? HPW : 0);
+        wait_vm(__builtin_amdgcn_readfirstlane(allow));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // every read of stage st returned
+      const int c = kt / 9, t = kt - 9 * c;
+      if (kt + S < nk) issueB(kt + S, st);
+      if (t == 8 && c + 2 < cend) issueH(c + 2);
+      const int st1 = st == S - 1 ? 0 : st + 1;
+      if (kt + 1 < nk) readF(S0{}, kt + 1, st1);
+      mma(S1{});
+      st = st1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else if constexpr (HALO == 1) {
     // ---- halo main loop: K step kt = (slab c = kt / 9, tap t = kt % 9), a slab = BK channels; host
     //      guarantees W = 2^lw in [16, kHaloWMax], BM % W == 0, H % (BM / W) == 0, C0 % BK == C1 % BK == 0,
     //      one split (kt0 = 0).
@@ -722,7 +850,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
   }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int BK, int S, bool HALO>
+template <typename T, int BM, int BN, int WM, int WN, int BK, int S, int HALO>
 void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, a.batch * sp.splits), block(WM * WN * 64);
@@ -733,11 +861,11 @@ void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
     nm = std::string("irx::(anonymous namespace)::gemm2_kernel<") + tn + ", " + std::to_string(BM) + ", " +
          std::to_string(BN) + ", " + std::to_string(WM) + ", " + std::to_string(WN) + ", " + std::to_string(BK) + ", " +
          std::to_string(S) + ", " + (a.conv ? "true" : "false") + ", " + (a.out_f32 ? "true" : "false") + ", " +
-         (rs ? "true" : "false") + ", " + (HALO ? "true" : "false") + ">";
+         (rs ? "true" : "false") + ", " + std::to_string(HALO) + ">";
   {
     ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
-    if constexpr (HALO) {
-      gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false, true><<<grid, block, 0, s>>>(a, sp);
+    if constexpr (HALO != 0) {
+      gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false, HALO><<<grid, block, 0, s>>>(a, sp);
     } else if (a.conv) {   // (fp32-output convs never take this path: see eligible())
       if (rs) gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, true><<<grid, block, 0, s>>>(a, sp);
       else gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false><<<grid, block, 0, s>>>(a, sp);
@@ -760,7 +888,7 @@ void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int S, bool HALO = false>
+template <int BM, int BN, int WM, int WN, int BK, int S, int HALO = 0>
 void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
   if (a.dtype == F16) launch2_t<f16_t, BM, BN, WM, WN, BK, S, HALO>(a, sp, s);
   else launch2_t<bf16_t, BM, BN, WM, WN, BK, S, HALO>(a, sp, s);
@@ -948,6 +1076,7 @@ size_t gemm_workspace_bytes(const GemmArgs& a) {
 // K splits of a halo conv (whole 64-channel slabs per split): 1 when the tiles fill the chip, 2 (in-kernel
 // reduction) when two splits do, 0 = the halo path does not take the shape.
 int g_halo_split = 1;   // irx_set_option("halo_split", 0): no K-split halo tiles (A/B)
+int g_halo_pipe = 1;    // irx_set_option("halo_pipe", 0): the round-2 halo main loop (A/B)
 
 int halo_splits(const GemmArgs& a, long tiles) {
   if (tiles >= kCUs || g_conv_halo >= 2) return 1;
@@ -998,7 +1127,8 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
       sp.inkernel = true;
       sp.cnt = stream_counters(s);
     }
-    launch2<256, 160, 4, 2, 64, 3, true>(b, sp, s);
+    if (g_halo_pipe && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 2>(b, sp, s);   // software-pipelined main loop
+    else launch2<256, 160, 4, 2, 64, 3, 1>(b, sp, s);
     return true;
   }
   const Choice c = choose(a);

@@ -154,6 +154,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 // ---------------------------------------------------------------- host-side errors
 void set_error(const std::string& msg);
+// rccl.cpp: in-place uint8 ncclBroadcast (librccl resolved at first use)
+void rccl_broadcast(void* comm, void* buf, size_t bytes, int root, hipStream_t s);
 const char* last_error();
 
 struct Error : public std::exception {

@@ -59,6 +59,7 @@ class Model {
   const std::vector<ParamEntry>& manifest() const { return params_; }
   size_t blob_bytes() const { return blob_bytes_; }
   void bind(void* blob, size_t bytes);
+  char* blob() const { return blob_; }   // the bound device blob (nullptr before bind)
 
  protected:
   P reg(const std::string& name, int layout, int dtype, std::vector<int64_t> shape, float row_scale = 1.f,

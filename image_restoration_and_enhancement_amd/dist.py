@@ -8,7 +8,9 @@ or gradient collectives; outputs stay on their rank (or are gathered once by the
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
+import sys
 from typing import Dict, Tuple
 
 import torch
@@ -48,6 +50,49 @@ def broadcast_blobs(blobs: Dict[str, torch.Tensor], src: int = 0) -> Dict[str, t
         for k in sorted(blobs):
             dist.broadcast(blobs[k], src=src)
     return blobs
+
+
+def rccl_comm(rank: int, world: int) -> C.c_void_p:
+    """The engine's own RCCL communicator on the current HIP device (irx_rccl_comm_init through the C ABI).
+    Rank 0 makes the 128-byte unique id; it reaches the other ranks over the torch.distributed rendezvous
+    (host plumbing only — the collectives themselves are RCCL calls inside libirx)."""
+    from . import _lib as L
+    idb = C.create_string_buffer(128)
+    if rank == 0:
+        L.call("irx_rccl_unique_id", idb)
+    obj = [idb.raw]
+    if world > 1:
+        dist.broadcast_object_list(obj, src=0)
+    comm = C.c_void_p()
+    L.call("irx_rccl_comm_init", obj[0], world, rank, C.byref(comm))
+    return comm
+
+
+def broadcast_models(models: Dict[str, object], src: int = 0) -> str:
+    """Broadcast every model's bound weight blob from `src` with irx_weights_bcast (RCCL over xGMI, in place,
+    on the current stream), name order.  Every rank must have bound a blob of the model's size.  Returns how
+    the weights moved: "none" (one rank), "irx_rccl", or — when the engine's RCCL cannot be initialised — the
+    torch.distributed broadcast of the same blobs, logged loudly and named in the return value."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return "none"
+    import torch
+    from . import _lib as L
+    rank, world = dist.get_rank(), dist.get_world_size()
+    try:
+        comm = rccl_comm(rank, world)
+    except L.IrxError as e:
+        print(f"[rank {rank}] irx RCCL unavailable ({e}); broadcasting weights with torch.distributed",
+              file=sys.stderr, flush=True)
+        broadcast_blobs({k: m.blob for k, m in models.items()}, src)
+        return f"torch.distributed ({e})"
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    try:
+        for k in sorted(models):
+            L.call("irx_weights_bcast", models[k].h, comm, src, s)
+        torch.cuda.current_stream().synchronize()
+    finally:
+        L.call("irx_rccl_comm_destroy", comm)
+    return "irx_rccl"
 
 
 def gather_shards(shard: torch.Tensor, n_total: int) -> torch.Tensor:

@@ -440,19 +440,23 @@ class RestorationPipeline:
                       max_batch: int = 8) -> List[Image.Image]:
         """Batched form of the single-image entry points (new; the reference loops one image per call).
         Images of equal processed size run as one engine batch of up to `max_batch`; each image gets the
-        result the single-image call returns (per-call reseeded noise) — bit-exactly on the fp32 engine; on
-        bf16 a different batch size may select another GEMM tiling / split-K, i.e. different rounding.  Falls back to the
-        single-image entry point per image whenever that one would not take the diffusion path."""
+        result the single-image call returns (per-call reseeded noise).  The result does not depend on the
+        batch an image shares: every tile / split-K / GroupNorm-chunking decision is made for a canonical
+        16-image batch of the per-image shape and GroupNorm partials are per image, so batch 8
+        == 3 + 5 bit for bit on every engine (tests/test_batch_invariance_gpu.py).  Falls back to the
+        single-image entry point per image (with the caller's prompt) whenever that one would not take the
+        diffusion path."""
         task = "sr" if task == "super_resolution" else task
         loader = {"denoise": self.load_denoise_model, "sr": self.load_sr_model,
                   "colorize": self.load_colorize_model, "inpaint": self.load_inpaint_model}[task]
         loader()
         model = self.models.get(task)
+        pk = {"prompt": prompt} if prompt else {}
         single = {"denoise": lambda im, mk: self.denoise(im, **({"strength": strength} if strength is not None
-                                                                else {})),
-                  "sr": lambda im, mk: self.super_resolve(im),
-                  "colorize": lambda im, mk: self.colorize(im),
-                  "inpaint": lambda im, mk: self.inpaint(im, mask=mk)}[task]
+                                                                else {}), **pk),
+                  "sr": lambda im, mk: self.super_resolve(im, **pk),
+                  "colorize": lambda im, mk: self.colorize(im, **pk),
+                  "inpaint": lambda im, mk: self.inpaint(im, mask=mk, **pk)}[task]
         masks = list(masks) if masks is not None else [None] * len(images)
         if not isinstance(model, NativeSDModel):
             return [single(im, mk) for im, mk in zip(images, masks)]

@@ -172,7 +172,10 @@ class SDEngine:
         if not self.use_graphs or not lat.is_cuda:
             return self._loop_body(lat, kv, plans, guidance, cfg_on, mask_l, masked_l,
                                    self._loop_buffers(lat, plans, cfg_on))
-        key = (tuple(lat.shape), tuple(kv.shape), bool(cfg_on), float(guidance), mask_l is not None,
+        # the graph bakes in the UNet weight-blob pointer: the bound blob is part of the key (and each entry holds a
+        # reference to it, so a rebind can neither replay stale weights nor let the old blob be freed under it)
+        key = (self.unet.blob.data_ptr(), tuple(lat.shape), tuple(kv.shape), bool(cfg_on), float(guidance),
+               mask_l is not None,
                tuple((p.t, p.mode, tuple(p.c), tuple(p.hw), p.e_div, p.e_mul, p.store_slot, tuple(p.hist),
                       p.x_from_cur, p.save_cur) for p in plans))
         cs = torch.cuda.current_stream(self.device)
@@ -214,8 +217,11 @@ class SDEngine:
         L.call("irx_graph_end", _stream(), C.byref(h))
         g["exec"] = h
         g["ws"] = self.unet._ws          # the workspace the graph's launches point into stays alive with it
+        g["blob"] = self.unet.blob       # ... and so do the weights they read
         while len(self._graphs) >= 4:                         # a few loop shapes per engine
             old = self._graphs.pop(next(iter(self._graphs)))
+            # a replay of the evicted exec may still be queued on this stream: drain it before destroying
+            torch.cuda.current_stream(self.device).synchronize()
             L.call("irx_graph_destroy", old["exec"])
         self._graphs[key] = g
         return g

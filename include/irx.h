@@ -208,6 +208,22 @@ int irx_colorize_lab_u8(void* stream, const uint8_t* img, long npix, const doubl
 /* cv2.medianBlur(img, 5) on uint8 [batch][H][W][C], C <= 4 (src != dst). */
 int irx_median_blur_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch, int H, int W, int C, int ksize);
 
+/* ---- multi-GPU: RCCL over xGMI (SURVEY.md §8b `irx_weights_bcast(handle, rcclComm)`, §8e) ----
+   The reference has no multi-device path (src/inference.py:52-57 picks one device; it stands in for
+   `pipe.to("cuda")` at src/inference.py:175-176 on every rank but the first).  One process per GPU: rank 0
+   creates the id, the caller ships its 128 bytes to the other ranks over any host channel (the torchrun
+   store), each rank creates its communicator on its current HIP device, and the packed weight blob bound to
+   a model is broadcast in place from `root`, enqueued on `stream`.  No per-step collectives exist. */
+#define IRX_RCCL_ID_BYTES 128
+int irx_rccl_available(void);                        /* 1 when librccl can be loaded, else 0 */
+int irx_rccl_unique_id(unsigned char* id);           /* id: IRX_RCCL_ID_BYTES bytes (ncclGetUniqueId) */
+int irx_rccl_comm_init(const unsigned char* id, int nranks, int rank, void** comm);   /* ncclCommInitRank */
+int irx_rccl_comm_destroy(void* comm);
+int irx_rccl_broadcast(void* comm, void* buf, size_t bytes, int root, void* stream);  /* in place, uint8 */
+/* broadcast the model's bound weight blob (irx_model_bind) from `root`; every rank must have bound a blob of
+   irx_model_blob_bytes first (non-root ranks: uninitialised memory that this call fills) */
+int irx_weights_bcast(irx_model* m, void* comm, int root, void* stream);
+
 /* ---- single-op entry points (parity tests, composition) ---- */
 int irx_op_conv2d(void* stream, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int hin, int win,
                   int hv, int wv, const void* weight, const float* bias, int cout, int kh, int kw, int stride,
@@ -222,7 +238,9 @@ size_t irx_op_group_norm_ws_bytes(int n, int hw, int groups);
 /* GroupNorm(+SiLU) of (x0 | x1) folded into a 3x3 / stride-1 / pad-1 conv's halo operand path (the form the
    UNet / VAE resnets run); bias / rowadd / residual as irx_op_conv2d.  Fails (IRX error) when the shape does
    not take the fused path: *fused reports whether it would (query with out == NULL, nothing launched).
-   ws: irx_op_group_norm_ws_bytes + n * (c0 + c1) * 8 bytes. */
+   ws: irx_op_gn_conv3_ws_bytes(n, h * w, groups, c0 + c1) bytes
+   (= round_up(n * (c0 + c1) * 8, 256) + irx_op_group_norm_ws_bytes). */
+size_t irx_op_gn_conv3_ws_bytes(int n, int hw, int groups, int channels);
 int irx_op_gn_conv3(void* stream, int dtype, const void* x0, const void* x1, int c0, int c1, int n, int h, int w,
                     int groups, float eps, const float* gamma, const float* beta, int silu, const void* weight,
                     const float* bias, int cout, const float* rowadd, long rowadd_ld, const void* residual,

@@ -21,6 +21,9 @@ CONVS = [  # (label, N, H, W, C0, C1, Cout, k, stride, up)
     ("conv640@32", 16, 32, 32, 640, 0, 640, 3, 1, None),
     ("conv1280@16", 16, 16, 16, 1280, 0, 1280, 3, 1, None),
     ("conv1280@8", 16, 8, 8, 1280, 0, 1280, 3, 1, None),
+    ("cat640+320->320@64", 16, 64, 64, 640, 320, 320, 3, 1, None),
+    ("cat320+320->320@64", 16, 64, 64, 320, 320, 320, 3, 1, None),
+    ("cat1280+1280->1280@16", 16, 16, 16, 1280, 1280, 1280, 3, 1, None),
     ("cat1280+640->640@32", 16, 32, 32, 1280, 640, 640, 3, 1, None),
     ("up1280@16->32", 16, 16, 16, 1280, 0, 1280, 3, 1, (32, 32)),
     ("vae512@128", 8, 128, 128, 512, 0, 512, 3, 1, None),
@@ -72,9 +75,10 @@ def main():
     L.load()
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
-    base = {"large_tiles": 1, "gemm_deep": 0, "gemm_small": 0, "tile_256x320": 1, "splitk_inkernel": 1}
+    base = {"large_tiles": 1, "gemm_deep": 0, "gemm_small": 0, "tile_256x320": 1, "splitk_inkernel": 1, "halo_pipe": 1}
     allv = {"s2": {}, "ring64": {"gemm_deep": 2}, "ring32": {"gemm_deep": 1}, "small": {"gemm_small": 1}, "4wave": {"large_tiles": 0},
-            "no320": {"tile_256x320": 0}, "redk": {"splitk_inkernel": 0}, "no320redk": {"tile_256x320": 0, "splitk_inkernel": 0}}
+            "no320": {"tile_256x320": 0}, "redk": {"splitk_inkernel": 0}, "no320redk": {"tile_256x320": 0, "splitk_inkernel": 0},
+            "halo1": {"halo_pipe": 0}, "halo2": {"halo_pipe": 1}}
     variants = [(v, allv[v]) for v in args.variants.split(",")]
 
     def setv(opts):

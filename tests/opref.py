@@ -88,7 +88,7 @@ def gn_conv3(x0, gamma, beta, eps, w_oihw, bias, groups=32, silu=True, x1=None, 
         return bool(fused.value)
     wk = w_oihw.permute(0, 2, 3, 1).contiguous().to(device=x0.device, dtype=x0.dtype)
     b = bias.float().to(x0.device).contiguous() if bias is not None else None
-    nb = L.load().irx_op_group_norm_ws_bytes(N, H * W, groups) + N * (C0 + C1) * 8 + 256
+    nb = L.load().irx_op_gn_conv3_ws_bytes(N, H * W, groups, C0 + C1)
     ws = torch.empty(nb, dtype=torch.uint8, device=x0.device)
     out = torch.empty((N, H, W, Co), dtype=x0.dtype, device=x0.device)
     L.call("irx_op_gn_conv3", S(), DT[x0.dtype], P(x0), P(x1), C0, C1, N, H, W, groups, float(eps), P(gamma),

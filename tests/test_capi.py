@@ -58,3 +58,12 @@ def test_error_path_without_gpu(lib):
 def test_missing_library_raises(tmp_path):
     with pytest.raises(L.IrxError):
         L.load(tmp_path / "libirx_missing.so", force=True)
+
+
+def test_rccl_entry_points_without_gpu(lib):
+    """The RCCL boundary resolves librccl lazily (dlopen) and reports errors through the status path."""
+    h = L.load()
+    assert L.call("irx_rccl_available") in (0, 1)
+    assert h.irx_weights_bcast(None, None, 0, None) != 0
+    assert b"null model" in h.irx_last_error()
+    assert h.irx_rccl_broadcast(None, None, 16, 0, None) != 0

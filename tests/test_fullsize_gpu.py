@@ -182,14 +182,7 @@ def _ref(task: str, sched: str, res: int, n_evals: int, seed: int):
 
 
 def _images(task, res, n, seed):
-    imgs = np.stack([MC.smooth_image(res, res, seed=seed + i) for i in range(n)])
-    if task == "colorize":
-        g = imgs.astype(np.float32) @ np.array([0.299, 0.587, 0.114], np.float32)
-        imgs = np.repeat(np.round(g).astype(np.uint8)[..., None], 3, axis=3)
-    masks = None
-    if task == "inpaint":
-        masks = np.stack([MC.stroke_mask(res, res, seed=seed + i) for i in range(n)]).astype(np.float32) / 255.0
-    return imgs, masks
+    return MC.task_images(task, res, n, seed)
 
 
 def _run_engine(eng, task, res, n, seed, n_evals, sched):

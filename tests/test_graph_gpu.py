@@ -51,3 +51,26 @@ def test_graph_replay_inpaint(device):
         o = eng.inpaint(img, mask, prompt, strength, 20, guidance)
     assert len(eng._graphs) == 1
     assert torch.equal(o.latents, eager.latents)
+
+
+def test_graph_rebind_weights_after_capture(device):
+    """a captured loop bakes in the UNet blob pointer.  Rebinding other weights after a capture must
+    give the new weights' result (a new graph), never a replay over the old (released) blob."""
+    prompt, strength, steps, guidance = PR.TASKS["denoise"]
+    imgs = torch.from_numpy(MC.smooth_image(64, 64, seed=71)[None]).to(device)
+    eng = _engine(device, "bf16", True)
+    for _ in range(2):
+        eng.img2img(imgs, prompt, strength, 20, guidance, seed=42)
+    assert len(eng._graphs) == 1
+    pc, _ = MC.state_dicts("denoise")
+    from image_restoration_and_enhancement_amd import weights as W
+    sd1 = W.random_state_dict("unet", pc.unet, 1)
+    eng.unet.load_state_dict(sd1)           # new blob; the old one may now only live on inside the graph entry
+    torch.cuda.empty_cache()
+    got = [eng.img2img(imgs, prompt, strength, 20, guidance, seed=42) for _ in range(2)]
+    ref = _engine(device, "bf16", False)
+    ref.unet.load_state_dict(sd1)
+    want = ref.img2img(imgs, prompt, strength, 20, guidance, seed=42)
+    assert len(eng._graphs) == 2
+    for o in got:
+        assert torch.equal(o.latents, want.latents)

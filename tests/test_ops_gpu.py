@@ -461,6 +461,41 @@ def test_conv_halo_split_k(device, case, dt):
     assert O.rel_err(got, ref) < TOL[dt]
 
 
+@pytest.mark.parametrize("case", [
+    # (N, H, W, C0, C1, Cout, forced): W 64 / 32 / 16, concat seams, the K-split 16x16 level (two in-kernel
+    # reduced splits), batch-16 production shapes; `forced` = halo tiles although the grid is small
+    (16, 64, 64, 320, 0, 320, False),
+    (4, 64, 64, 640, 320, 320, False),
+    (16, 32, 32, 640, 0, 640, False),
+    (2, 16, 32, 128, 64, 160, True),
+    (16, 16, 16, 1280, 1280, 1280, False),
+    (1, 16, 16, 64, 64, 160, True),
+])
+@pytest.mark.parametrize("dt", DT16)
+def test_conv_halo_pipelined_bit_exact(device, case, dt):
+    """The software-pipelined halo main loop (option halo_pipe, default) issues the same MFMAs into every
+    accumulator in the same order as the round-2 loop: outputs are identical bit for bit."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    N, H, W, C0, C1, Co, forced = case
+    x0 = _dev(_r(N, H, W, C0, seed=280), dt, device)
+    x1 = _dev(_r(N, H, W, C1, seed=281), dt, device) if C1 else None
+    w = _r(Co, C0 + C1, 3, 3, seed=282, scale=1 / math.sqrt((C0 + C1) * 9))
+    b = _r(Co, seed=283)
+    temb = _r(N, Co, seed=284).to(device).contiguous()
+    res = _dev(_r(N, H, W, Co, seed=285), dt, device)
+    L.call("irx_set_option", b"conv_halo", 2 if forced else 1)
+    try:
+        outs = []
+        for pipe in (0, 1):
+            L.call("irx_set_option", b"halo_pipe", pipe)
+            outs.append(O.conv2d(x0, w.to(dt).float(), b, x1=x1, rowadd=temb, residual=res))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1])
+    finally:
+        L.call("irx_set_option", b"halo_pipe", 1)
+        L.call("irx_set_option", b"conv_halo", 1)
+
+
 @pytest.mark.parametrize("B,L", [(2, 256), (1, 333), (2, 1024), (1, 77)])
 @pytest.mark.parametrize("dt", DT16)
 def test_attention_d512_flash(device, dt, B, L):
