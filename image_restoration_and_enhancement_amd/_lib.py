@@ -16,6 +16,7 @@ IRX_F32, IRX_BF16, IRX_F16 = 0, 1, 2
 IRX_MODEL_UNET, IRX_MODEL_VAE, IRX_MODEL_CLIP = 0, 1, 2
 IRX_LAYOUT_VEC, IRX_LAYOUT_MAT, IRX_LAYOUT_CONV, IRX_LAYOUT_EMB = 0, 1, 2, 3
 IRX_LAYOUT_MAT_GEGLU64, IRX_LAYOUT_VEC_GEGLU64 = 4, 5
+IRX_LAYOUT_VEC_LN_U, IRX_LAYOUT_VEC_LN_V = 6, 7
 
 
 class IrxError(RuntimeError):
@@ -38,7 +39,7 @@ class ModelConfig(C.Structure):
 class ParamInfo(C.Structure):
     _fields_ = [("name", C.c_char_p), ("layout", C.c_int), ("dtype", C.c_int), ("ndim", C.c_int),
                 ("shape", C.c_int64 * 4), ("offset", C.c_size_t), ("bytes", C.c_size_t),
-                ("row_scale", C.c_float), ("scale_rows", C.c_int64)]
+                ("row_scale", C.c_float), ("scale_rows", C.c_int64), ("aux", C.c_char_p)]
 
 
 class StepParams(C.Structure):

@@ -68,6 +68,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gn_parts") g_gn_parts = value;
   else if (n == "halo_split") g_halo_split = value;
   else if (n == "halo_pipe") g_halo_pipe = value;
+  else if (n == "ln_fold") g_ln_fold = value;
   else if (n == "vae_attn_rows") g_vae_attn_rows = value;
   else if (n == "vae_flash") g_vae_flash = value;
   else if (n == "splitk_inkernel") g_splitk_inkernel = value != 0;
@@ -197,6 +198,7 @@ int irx_model_param_info(const irx_model* m, int i, irx_param_info* info) {
   info->bytes = e.bytes;
   info->row_scale = e.row_scale;
   info->scale_rows = e.scale_rows;
+  info->aux = e.aux.c_str();
   IRX_API_END
 }
 

@@ -280,8 +280,13 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   } else {
     IRX_CHECK(a.A && a.lda % vec == 0 && ((uintptr_t)a.A % 16) == 0, "A rows must be 16-byte aligned");
   }
+  IRX_CHECK(!a.ln_rs || (a.ln_u && gemm_ln_foldable(a)), "folded LayerNorm needs the large-tile path");
   if (a.geglu) {
     IRX_CHECK(gemm_geglu_fusable(a) && gemm_large_tile(a, s), "GEGLU epilogue needs the large-tile path");
+    return;
+  }
+  if (a.ln_rs) {
+    IRX_CHECK(gemm_large_tile(a, s), "folded LayerNorm needs the large-tile path");
     return;
   }
   if (a.gn_part) {

@@ -238,54 +238,66 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   };
 
   if constexpr (HALO == 2) {
-    // ---- software-pipelined halo main loop (the default halo path; no GroupNorm-fused operand).  A K step
-    //      (slab c = kt / 9, tap t = kt % 9) is two 32-deep sub-steps; the fragments of sub-step 1 are read
-    //      while sub-step 0's MFMAs run, and those of the NEXT step's sub-step 0 right after the barrier, under
-    //      sub-step 1's MFMAs: no wave ever waits on an LDS read at the head of a step (the form above requests
-    //      all of a step's fragments after the barrier and then stalls on them while all 8 waves flood the LDS).
-    //      B ring of S = 3 stages, two steps ahead: before the barrier of step kt every wave drains its reads
-    //      (lgkmcnt(0)), so after it the DMA of step kt+3 may overwrite step kt's stage.  Halo buffers: slab
-    //      c+2's halo is issued after the barrier of slab c's last tap (when every read of slab c's buffer has
-    //      returned) and has nine steps to land.  Every wave issues IPB B pieces and HPW halo pieces per issue
-    //      (surplus ones land in a scratch KiB), so one counted vmcnt per step covers both streams.
-    static_assert(S == 3 && KSUB == 2, "pipelined halo: 3-stage B ring, BK 64");
+    // ---- ping-pong halo main loop (the default halo path; no GroupNorm-fused operand).  The two waves that
+    //      share a SIMD (w and w + 4) take opposite roles in each half of a K step (slab c = kt / 9, tap
+    //      t = kt % 9), so one of them always has MFMAs to issue while the other moves data:
+    //        phase 1 of step kt: group 0 (waves 0-3) runs the 40 MFMAs of step kt on fragments it read in the
+    //                            previous phase; group 1 (waves 4-7) issues the LDS-DMA of B(kt + 2) and reads
+    //                            its own fragments of step kt;
+    //        phase 2 of step kt: group 1 runs its MFMAs of step kt; group 0 reads its fragments of step kt + 1
+    //                            and issues one sixth of a later slab's halo.
+    //      (the lock-step form, HALO == 1, issues DMA and fragment reads in both waves of a SIMD at once, and
+    //      the matrix pipe idles meanwhile.)  B ring of S = 3 stages: B(kt + 2) goes into the stage of
+    //      step kt - 1, which group 1 finished reading before the barrier that ended phase 1 of kt - 1 and
+    //      group 0 before it ran step kt - 1's MFMAs; group 1 waits for B(kt + 1) at the end of phase 1 of
+    //      kt, where group 0 needs it.  Halo buffers: slab c + 2's halo is issued by group 0 in six parts in
+    //      phase 2 of steps 9c + 8 .. 9c + 13 (slab c's buffer is free once phase 1 of its last tap is over)
+    //      and waited for (vmcnt(0): group 0 issues nothing else) at the end of phase 1 of the step before
+    //      slab c + 2 starts.
+    static_assert(S == 3 && KSUB == 2 && NW == 8, "ping-pong halo: 3-stage B ring, BK 64, 8 waves");
     const int W = a.g.Win, H = a.g.Hin, lw = __builtin_ctz(W);
     const int HW = H * W;
     const int img = m0 / HW, y0 = (m0 - img * HW) >> lw;
     const int nhi = (((BM >> lw) + 2) << lw) / RPI;   // halo wave-instructions (RPI pixel rows each)
-    constexpr int HPW = (BM + 2 * kHaloWMax) / RPI / NW;
-    static_assert(HPW * RPI * NW == BM + 2 * kHaloWMax, "uniform halo pieces per wave");
+    constexpr int NG = NW / 2;                        // waves per group
+    constexpr int HPG = (BM + 2 * kHaloWMax) / RPI / NG;   // halo pieces per group-0 wave per slab
+    constexpr int HPARTS = 6, HPP = HPG / HPARTS;          // ... issued in 6 parts
+    static_assert(HPG * RPI * NG == BM + 2 * kHaloWMax && HPP * HPARTS == HPG, "halo pieces");
+    constexpr int NBI = BN / RPI, BPG = NBI / NG;          // B wave-instructions per step, per group-1 wave
+    static_assert(BPG * NG == NBI, "B pieces");
+    const int wv = __builtin_amdgcn_readfirstlane(wave);   // (scalar: the role branches stay uniform)
+    const bool g1 = wv >= NG;
+    const int gw = wv - (g1 ? NG : 0);
     uint4* const Hb = smem;                           // [2][HB_U4]
     uint4* const Bsm = smem + 2 * HB_U4;              // [S][BN * CPR]
     uint4* const zrow = Bsm + S * BN * CPR;           // one zero pixel row: taps left / right of the image
     uint4* const scratch = zrow + CPR;                // 1 KiB target of the surplus pieces
     if (tid < CPR) zrow[tid] = uint4{0u, 0u, 0u, 0u};
     auto swz = [](int r) { return CPR == 8 ? (r & 7) : (((r >> 2) & 1) << 1); };
-    constexpr int NBI = BN / RPI, IPB = (NBI + NW - 1) / NW;
-    const uint16_t* bro[IPB];
+    const uint16_t* bro[BPG];
 #pragma unroll
-    for (int j = 0; j < IPB; ++j) {
-      const int q = wave * IPB + j, r = RPI * q + lane / CPR;
-      bro[j] = (q < NBI && n0 + r < a.N) ? Bp + (long)(n0 + r) * a.ldb + (((lane % CPR) ^ swz(r)) * 8) : nullptr;
+    for (int j = 0; j < BPG; ++j) {
+      const int q = gw * BPG + j, r = RPI * q + lane / CPR;
+      bro[j] = n0 + r < a.N ? Bp + (long)(n0 + r) * a.ldb + (((lane % CPR) ^ swz(r)) * 8) : nullptr;
     }
-    auto issueB = [&](int kt, int st) {
+    auto issueB = [&](int kt) {   // group 1: all of B(kt)
       const int c = kt / 9, t = kt - 9 * c;
       const int off = t * Cin + c * BK;
+      uint4* const st = Bsm + (kt % S) * BN * CPR;
 #pragma unroll
-      for (int j = 0; j < IPB; ++j) {
-        const int q = wave * IPB + j;
-        uint4* dst = q < NBI ? Bsm + st * BN * CPR + q * 64 : scratch;
+      for (int j = 0; j < BPG; ++j) {
+        uint4* dst = st + (gw * BPG + j) * 64;
         glds16_asm(bro[j] ? bro[j] + off : zp, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
       }
     };
-    auto issueH = [&](int c) {
+    auto issueH = [&](int c, int j0, int j1) {   // group 0: pieces [j0, j1) of slab c's halo
       const bool second = c * BK >= a.g.C0;
       const uint16_t* sb = second ? (const uint16_t*)a.g.src1 : (const uint16_t*)a.g.src0;
       const int cs = second ? a.g.C1 : a.g.C0;
       const int ch = second ? c * BK - a.g.C0 : c * BK;
-#pragma unroll
-      for (int j = 0; j < HPW; ++j) {
-        const int q = wave * HPW + j;
+#pragma unroll 1
+      for (int j = j0; j < j1; ++j) {
+        const int q = gw * HPG + j;
         const int p = RPI * q + lane / CPR;
         const int y = y0 - 1 + (p >> lw), x = p & (W - 1);
         const bool ok = q < nhi && y >= 0 && y < H;
@@ -295,73 +307,75 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       }
     };
     uint4 fa[KSUB][TM], fb[KSUB][TN];
-    // fragments of sub-step SS of K step kt (B stage st)
-    auto readF = [&](auto ss_c, int kt, int st) {
-      constexpr int SS = decltype(ss_c)::value;
+    auto readF = [&](int kt) {   // this wave's fragments of step kt (both 32-deep sub-steps)
       const int c = kt / 9, t = kt - 9 * c;
       const int ky = t / 3, kx = t - 3 * ky;
       const int shift = ky * W + kx - 1;
       const uint4* Hs = Hb + (c & 1) * HB_U4;
-      const uint4* Bs = Bsm + st * BN * CPR;
-      const int ck = SS * 4 + fgrp;
+      const uint4* Bs = Bsm + (kt % S) * BN * CPR;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int r = wm * TM * 16 + i * 16 + frow;
-        const int rx = r & (W - 1);
-        const int hp = r + shift;
-        const bool zero = (kx == 0 && rx == 0) || (kx == 2 && rx == W - 1);
-        fa[SS][i] = zero ? zrow[ck] : Hs[hp * CPR + (ck ^ swz(hp))];
-      }
+      for (int ss = 0; ss < KSUB; ++ss) {
+        const int ck = ss * 4 + fgrp;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int r = wn * TN * 16 + j * 16 + frow;
-        fb[SS][j] = Bs[r * CPR + (ck ^ swz(r))];
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * TM * 16 + i * 16 + frow;
+          const int rx = r & (W - 1);
+          const int hp = r + shift;
+          const bool zero = (kx == 0 && rx == 0) || (kx == 2 && rx == W - 1);
+          fa[ss][i] = zero ? zrow[ck] : Hs[hp * CPR + (ck ^ swz(hp))];
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * TN * 16 + j * 16 + frow;
+          fb[ss][j] = Bs[r * CPR + (ck ^ swz(r))];
+        }
       }
     };
-    auto mma = [&](auto ss_c) {
-      constexpr int SS = decltype(ss_c)::value;
+    auto mma = [&]() {
       if (a.dbg & 2) return;
-      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int ss = 0; ss < KSUB; ++ss)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[SS][i], fb[SS][j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[ss][i], fb[ss][j], acc[i][j]);
     };
-    using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
+    auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
     // this split's K steps [kt0, nk): whole slabs (host: sp.per is a multiple of 9); >= 9 steps per split
     const int nk = kt1, c0 = kt0 / 9, cend = (kt1 + 8) / 9;
-    const bool h1 = c0 + 1 < cend;
-    // halo issued "at step i" (after B(i + 3)): the prologue's H(c0 + 1) counts as step kt0 - 1
-    auto hasH = [&](int i) {
-      return i == kt0 - 1 ? h1 : (i >= kt0 && i - 9 * (i / 9) == 8 && i / 9 + 2 < cend);
-    };
-    issueH(c0);
-#pragma unroll
-    for (int p = 0; p < S; ++p) issueB(kt0 + p, p);
-    if (h1) issueH(c0 + 1);
-    wait_vm(2 * IPB + (h1 ? HPW : 0));                  // H(c0) and B(kt0) landed
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // (+ the zero row)
-    readF(S0{}, kt0, 0);
-    int st = 0;
-    for (int kt = kt0; kt < nk; ++kt) {
-      readF(S1{}, kt, st);
-      mma(S0{});
-      if (kt + 1 < nk) {
-        // younger than B(kt+1): B(kt+2), and a halo issued at step kt-1 or kt-2
-        const int allow = (kt + 2 < nk ? IPB : 0) + ((hasH(kt - 1) || hasH(kt - 2)) ? HPW : 0);
-        wait_vm(__builtin_amdgcn_readfirstlane(allow));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // every read of stage st returned
-      const int c = kt / 9, t = kt - 9 * c;
-      if (kt + S < nk) issueB(kt + S, st);
-      if (t == 8 && c + 2 < cend) issueH(c + 2);
-      const int st1 = st == S - 1 ? 0 : st + 1;
-      if (kt + 1 < nk) readF(S0{}, kt + 1, st1);
-      mma(S1{});
-      st = st1;
+    if (g1) {
+      issueB(kt0);
+      issueB(kt0 + 1);
+      wait_vm(BPG);                                      // B(kt0) landed
+    } else {
+      issueH(c0, 0, HPG);
+      if (c0 + 1 < cend) issueH(c0 + 1, 0, HPG);
+      wait_vm(c0 + 1 < cend ? HPG : 0);                   // H(c0) landed
     }
+    barrier();                                           // (+ the zero row)
+    // one program for both groups: every wave runs {load phase of step k; barrier; compute phase of step k;
+    // barrier}, group 1 one phase behind group 0 (one extra barrier in front, group 0 one extra at the end),
+    // so each interval between barriers pairs one group's MFMAs with the other group's loads
+    if (g1) barrier();
+    for (int kt = kt0; kt < nk; ++kt) {
+      const int c = kt / 9, t = kt - 9 * c;
+      // ---- load phase
+      if (g1) {
+        if (kt + 2 < nk) issueB(kt + 2);
+      } else if (kt > kt0) {   // the halo part scheduled after step kt - 1
+        const int cp = (kt - 1) / 9, tp = kt - 1 - 9 * cp;
+        if (tp == 8 && cp + 2 < cend) issueH(cp + 2, 0, HPP);
+        else if (tp < HPARTS - 1 && cp > c0 && cp + 1 < cend) issueH(cp + 1, (tp + 1) * HPP, (tp + 2) * HPP);
+      }
+      readF(kt);
+      if (g1 && kt + 1 < nk) wait_vm(kt + 2 < nk ? BPG : 0);   // B(kt + 1) landed (group 0 reads it next)
+      barrier();
+      // ---- compute phase
+      mma();
+      if (!g1 && t == 8 && c + 1 < cend) wait_vm(0);              // the next slab's halo landed
+      barrier();
+    }
+    if (!g1) barrier();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   } else if constexpr (HALO == 1) {
@@ -621,18 +635,42 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       constexpr int CPR = BN / 8;               // 16-byte chunks per row
       // chunk swizzle inside whole groups of 8 chunks only (BN = 160 leaves a 4-chunk tail unswizzled)
       auto csw = [](int c, int row) { return c < (CPR & ~7) ? c ^ (row & 7) : c; };
+      if (a.ln_rs) {
+        // folded LayerNorm (GemmArgs::ln_rs): y = rstd * acc - rstd * mean * u[n] + bias[n]  (alpha == 1)
+        float uu[TN], bb[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = wn * TN * 16 + j * 16 + frow;
-        const float bias = (a.bias && n0 + col < a.N) ? a.bias[n0 + col] : 0.f;
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * TN * 16 + j * 16 + frow;
+          uu[j] = n < a.N ? a.ln_u[n] : 0.f;
+          bb[j] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = wm * TM * 16 + i * 16 + fgrp * 4 + r;
-            tileS[row * BN + (csw(col >> 3, row) << 3) + (col & 7)] =
-                __builtin_bit_cast(uint16_t, from_f<T>(acc[i][j][r] * a.alpha + bias));
+            const float2 rs = m0 + row < a.M ? a.ln_rs[m0 + row] : make_float2(0.f, 0.f);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const int col = wn * TN * 16 + j * 16 + frow;
+              tileS[row * BN + (csw(col >> 3, row) << 3) + (col & 7)] =
+                  __builtin_bit_cast(uint16_t, from_f<T>(fmaf(acc[i][j][r], rs.x, fmaf(-rs.y, uu[j], bb[j]))));
+            }
           }
+      } else {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = wn * TN * 16 + j * 16 + frow;
+          const float bias = (a.bias && n0 + col < a.N) ? a.bias[n0 + col] : 0.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = wm * TM * 16 + i * 16 + fgrp * 4 + r;
+              tileS[row * BN + (csw(col >> 3, row) << 3) + (col & 7)] =
+                  __builtin_bit_cast(uint16_t, from_f<T>(acc[i][j][r] * a.alpha + bias));
+            }
+        }
       }
       __syncthreads();
       if (a.geglu) {
@@ -1052,6 +1090,20 @@ int gemm_emits_gn_parts(const GemmArgs& a) {
   return c.BM;
 }
 
+int g_ln_fold = 1;
+
+bool gemm_ln_foldable(const GemmArgs& a) {
+  if (!g_large_tiles || !is16(a.dtype) || a.conv || a.alpha != 1.f || a.out_f32 || a.batch != 1) return false;
+  if (!eligible(a) || !vec_ok(a)) return false;
+  const Choice c = choose(a);
+  if (c.BM == 0) return false;
+  if (c.splits > 1) {   // only the in-kernel reduction runs the full epilogue
+    const long tiles = (long)((a.M + c.BM - 1) / c.BM) * ((a.N + c.BN - 1) / c.BN);
+    if (!(g_splitk_inkernel && c.splits == 2 && tiles <= kSplitCounters)) return false;
+  }
+  return true;
+}
+
 bool gemm_geglu_fusable(const GemmArgs& a) {
   if (!g_large_tiles || !a.geglu || !eligible(a) || !vec_ok(a)) return false;
   return choose(a).BM != 0;
@@ -1109,6 +1161,7 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   if (!eligible(a)) return false;
   IRX_CHECK(!a.gn_ab || halo_bn(a), "GroupNorm-fused operand needs the halo conv path");
   IRX_CHECK(!a.gn_part || gemm_emits_gn_parts(a), "GroupNorm partials need the large-tile epilogue");
+  IRX_CHECK(!a.ln_rs || gemm_ln_foldable(a), "folded LayerNorm needs the large-tile epilogue");
   if (const int hbn = halo_bn(a)) {
     GemmArgs b = a;
     b.vec_epilogue = 1;

@@ -63,10 +63,10 @@ void Arena::free(void* p) {
 
 // ---------------------------------------------------------------------------------------------- Model
 P Model::reg(const std::string& name, int layout, int dtype, std::vector<int64_t> shape, float row_scale,
-            int64_t scale_rows) {
+            int64_t scale_rows, const std::string& aux) {
   int64_t n = 1;
   for (auto d : shape) n *= d;
-  ParamEntry e{name, layout, dtype, shape, blob_bytes_, (size_t)n * dsize(dtype), row_scale, scale_rows};
+  ParamEntry e{name, layout, dtype, shape, blob_bytes_, (size_t)n * dsize(dtype), row_scale, scale_rows, aux};
   params_.push_back(e);
   P p;
   p.off = blob_bytes_;
@@ -235,11 +235,22 @@ Unet::XfW Unet::make_xf(const std::string& p, int c) {
   // kernel's exp2 then needs no multiply per score)
   const bool fold = dt_ != F32;
   const float qs = fold ? 1.4426950408889634f / std::sqrt((float)(c / cfg_.heads)) : 1.f;
-  a.qkvw = reg(b + "attn1.to_q.weight|" + b + "attn1.to_k.weight|" + b + "attn1.to_v.weight", IRX_LAYOUT_MAT, dt_,
-               {3 * c, c}, qs, fold ? c : 0);
+  // LayerNorm fold (ln_fold_): each LN's gamma scales the columns of the projection it feeds, and the packer adds
+  // u = row sums of the packed matrix and v = bias + W beta (layouts IRX_LAYOUT_VEC_LN_U / _LN_V)
+  const bool lnf = ln_fold_;
+  const std::string qkv = b + "attn1.to_q.weight|" + b + "attn1.to_k.weight|" + b + "attn1.to_v.weight";
+  a.qkvw = reg(qkv, IRX_LAYOUT_MAT, dt_, {3 * c, c}, qs, fold ? c : 0, lnf ? b + "norm1.weight" : "");
+  if (lnf) {
+    a.qkvu = reg(qkv, IRX_LAYOUT_VEC_LN_U, F32, {3 * c});
+    a.qkvv = reg(qkv, IRX_LAYOUT_VEC_LN_V, F32, {3 * c}, 1.f, 0, b + "norm1.bias;");
+  }
   a.o1w = mat(b + "attn1.to_out.0.weight", c, c); a.o1b = vec(b + "attn1.to_out.0.bias", c);
   a.ln2w = vec(b + "norm2.weight", c); a.ln2b = vec(b + "norm2.bias", c);
-  a.q2w = reg(b + "attn2.to_q.weight", IRX_LAYOUT_MAT, dt_, {c, c}, qs, fold ? c : 0);
+  a.q2w = reg(b + "attn2.to_q.weight", IRX_LAYOUT_MAT, dt_, {c, c}, qs, fold ? c : 0, lnf ? b + "norm2.weight" : "");
+  if (lnf) {
+    a.q2u = reg(b + "attn2.to_q.weight", IRX_LAYOUT_VEC_LN_U, F32, {c});
+    a.q2v = reg(b + "attn2.to_q.weight", IRX_LAYOUT_VEC_LN_V, F32, {c}, 1.f, 0, b + "norm2.bias;");
+  }
   a.kv_off = kv_cols_;
   kv_cols_ += 2 * c;
   kv_names_.push_back(b + "attn2.to_k.weight");
@@ -247,8 +258,13 @@ Unet::XfW Unet::make_xf(const std::string& p, int c) {
   a.o2w = mat(b + "attn2.to_out.0.weight", c, c); a.o2b = vec(b + "attn2.to_out.0.bias", c);
   a.ln3w = vec(b + "norm3.weight", c); a.ln3b = vec(b + "norm3.bias", c);
   // GEGLU projection rows interleaved in (64 value, 64 gate) blocks so one output tile holds both halves
-  a.ffw = reg(b + "ff.net.0.proj.weight", IRX_LAYOUT_MAT_GEGLU64, dt_, {8 * c, c});
+  const std::string ff = b + "ff.net.0.proj.weight";
+  a.ffw = reg(ff, IRX_LAYOUT_MAT_GEGLU64, dt_, {8 * c, c}, 1.f, 0, lnf ? b + "norm3.weight" : "");
   a.ffb = reg(b + "ff.net.0.proj.bias", IRX_LAYOUT_VEC_GEGLU64, F32, {8 * c});
+  if (lnf) {
+    a.ffu = reg(ff, IRX_LAYOUT_VEC_LN_U, F32, {8 * c});
+    a.ffv = reg(ff, IRX_LAYOUT_VEC_LN_V, F32, {8 * c}, 1.f, 0, b + "norm3.bias;" + b + "ff.net.0.proj.bias");
+  }
   a.ff2w = mat(b + "ff.net.2.weight", c, 4 * c); a.ff2b = vec(b + "ff.net.2.bias", c);
   a.pow = mat(p + "proj_out.weight", c, c); a.pob = vec(p + "proj_out.bias", c);
   return a;
@@ -260,6 +276,7 @@ Unet::Unet(const irx_model_config& cfg, int dtype) : Model(IRX_MODEL_UNET, cfg, 
   const int* bo = cfg.block_out_channels;
   const int nb = cfg.n_blocks;
   cin_pad_ = (cfg.in_channels + 7) / 8 * 8;
+  ln_fold_ = dtype != F32 && g_ln_fold;
   temb_dim_ = bo[0] * 4;
   conv_in_w = conv("conv_in.weight", bo[0], 3, 3, cin_pad_);
   conv_in_b = vec("conv_in.bias", bo[0]);
@@ -341,6 +358,30 @@ Act Unet::resnet(Ctx& c, const ResW& r, Act& x0, Act* x1, const float* tproj, fl
   return out;
 }
 
+void Unet::ln_gemm(Ctx& c, GemmArgs& g, const void* x, int rows, int C, P lnw, P lnb, P u, P v, const float* bias,
+                   void* nbuf, float2* st) {
+  g.lda = C;
+  if (!ln_fold_) {
+    lnorm(c, x, rows, C, lnw, lnb, 1e-5f, nbuf);
+    g.A = nbuf;
+    g.bias = bias;
+  } else {
+    g.bias = fptr(v);                 // bias + W beta
+    g.A = x;
+    g.ln_rs = st;
+    g.ln_u = fptr(u);
+    if (gemm_ln_foldable(g)) {
+      if (!c.ws->dry()) layer_norm_stats(dt_, x, C, rows, C, 1e-5f, st, c.s);
+    } else {                          // (W * gamma, bias + W beta) after an affine-free LayerNorm
+      g.ln_rs = nullptr;
+      g.ln_u = nullptr;
+      if (!c.ws->dry()) layer_norm(dt_, x, C, rows, C, 1e-5f, nullptr, nullptr, nbuf, C, c.s);
+      g.A = nbuf;
+    }
+  }
+  run_gemm(c, g);
+}
+
 Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   const int B = x.n, HW = x.h * x.w, C = a.c;
   const long M = (long)B * HW;
@@ -354,7 +395,7 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   drop(c, gn);
   void* n = c.ws->alloc(M * C * es);
   void* att = c.ws->alloc(M * C * es);
-  lnorm(c, h.p, M, C, a.ln1w, a.ln1b, 1e-5f, n);
+  float2* st = ln_fold_ ? (float2*)c.ws->alloc(M * sizeof(float2)) : nullptr;   // LayerNorm row statistics
   // self-attention
   void* qkv = c.ws->alloc(M * 3 * C * es);
   // 16-bit engines: q|k|v written head-major ([q|k|v][image][head][token][d], GemmArgs::hs_*) so each attention
@@ -363,10 +404,10 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   {
     GemmArgs g;
     g.dtype = dt_; g.M = M; g.N = 3 * C; g.K = C;
-    g.A = n; g.lda = C; g.B = ptr(a.qkvw); g.ldb = C;
+    g.B = ptr(a.qkvw); g.ldb = C;
     g.C = qkv; g.ldc = 3 * C; g.imgs = B;
     if (hm) { g.hs_L = HW; g.hs_C = C; g.hs_d = d; }
-    run_gemm(c, g);
+    ln_gemm(c, g, h.p, M, C, a.ln1w, a.ln1b, a.qkvu, a.qkvv, nullptr, n, st);
   }
   if (!c.ws->dry()) {
     AttnArgs aa;
@@ -387,15 +428,14 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   }
   c.ws->free(qkv);
   linear(c, att, C, M, C, a.o1w, C, fptr(a.o1b), h.p, C, ACT_NONE, h.p, C, 0, B);
-  lnorm(c, h.p, M, C, a.ln2w, a.ln2b, 1e-5f, n);
   // cross-attention (K|V precomputed per prompt)
   {
     GemmArgs g;
     g.dtype = dt_; g.M = M; g.N = C; g.K = C;
-    g.A = n; g.lda = C; g.B = ptr(a.q2w); g.ldb = C;
+    g.B = ptr(a.q2w); g.ldb = C;
     g.C = att; g.ldc = C; g.imgs = B;
     if (hm) { g.hs_L = HW; g.hs_C = C; g.hs_d = d; }
-    run_gemm(c, g);
+    ln_gemm(c, g, h.p, M, C, a.ln2w, a.ln2b, a.q2u, a.q2v, nullptr, n, st);
   }
   if (!c.ws->dry()) {
     AttnArgs aa;
@@ -409,27 +449,28 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     attention(aa, c.s);
   }
   linear(c, n, C, M, C, a.o2w, C, fptr(a.o2b), h.p, C, ACT_NONE, h.p, C, 0, B);
-  lnorm(c, h.p, M, C, a.ln3w, a.ln3b, 1e-5f, n);
   // GEGLU feed-forward: fused into the projection's epilogue when the large-tile path takes the shape
   void* g = c.ws->alloc(M * 4 * C * es);
   {
     GemmArgs ga;
     ga.dtype = dt_; ga.M = M; ga.N = 8 * C; ga.K = C;
-    ga.A = n; ga.lda = C; ga.B = ptr(a.ffw); ga.ldb = C;
-    ga.C = g; ga.ldc = 4 * C; ga.bias = fptr(a.ffb); ga.geglu = 1;
+    ga.B = ptr(a.ffw); ga.ldb = C;
+    ga.C = g; ga.ldc = 4 * C; ga.geglu = 1;
     ga.imgs = B;
+    ga.A = h.p; ga.lda = C;
     if (gemm_geglu_fusable(ga)) {
-      run_gemm(c, ga);
+      ln_gemm(c, ga, h.p, M, C, a.ln3w, a.ln3b, a.ffu, a.ffv, fptr(a.ffb), n, st);
     } else {
       void* ff = c.ws->alloc(M * 8 * C * es);
       ga.geglu = 0; ga.C = ff; ga.ldc = 8 * C;
-      run_gemm(c, ga);
+      ln_gemm(c, ga, h.p, M, C, a.ln3w, a.ln3b, a.ffu, a.ffv, fptr(a.ffb), n, st);
       if (!c.ws->dry()) geglu(dt_, ff, 8 * C, M, 4 * C, g, 4 * C, 1, c.s);
       c.ws->free(ff);
     }
   }
   linear(c, g, 4 * C, M, 4 * C, a.ff2w, C, fptr(a.ff2b), h.p, C, ACT_NONE, h.p, C, 0, B);
   c.ws->free(g);
+  if (st) c.ws->free(st);
   c.ws->free(att);
   c.ws->free(n);
   Act out = new_act(c, B, x.h, x.w, C);

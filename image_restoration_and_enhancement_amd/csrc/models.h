@@ -40,6 +40,7 @@ struct ParamEntry {
   size_t off, bytes;
   float row_scale = 1.f;     // packer scales rows [0, scale_rows) (folded attention scale)
   int64_t scale_rows = 0;
+  std::string aux;           // irx_param_info::aux (LayerNorm fold sources)
 };
 
 struct Act {   // NHWC activation view
@@ -63,7 +64,7 @@ class Model {
 
  protected:
   P reg(const std::string& name, int layout, int dtype, std::vector<int64_t> shape, float row_scale = 1.f,
-        int64_t scale_rows = 0);
+        int64_t scale_rows = 0, const std::string& aux = std::string());
   P vec(const std::string& name, int64_t n) { return reg(name, IRX_LAYOUT_VEC, F32, {n}); }
   P mat(const std::string& name, int64_t n, int64_t k) { return reg(name, IRX_LAYOUT_MAT, dt_, {n, k}); }
   P conv(const std::string& name, int64_t co, int64_t kh, int64_t kw, int64_t ci) {
@@ -128,6 +129,9 @@ class Unet : public Model {
   struct XfW {
     P nw, nb, piw, pib, ln1w, ln1b, qkvw, o1w, o1b, ln2w, ln2b, q2w, o2w, o2b, ln3w, ln3b, ffw, ffb, ff2w, ff2b, pow,
         pob;
+    // LayerNorm fold (16-bit engines, ln_fold_): qkvw / q2w / ffw hold W * gamma; u = row sums of those, v = bias +
+    // W beta (GemmArgs::ln_rs / ln_u)
+    P qkvu, qkvv, q2u, q2v, ffu, ffv;
     int c = 0;
     long kv_off = 0;      // column offset into the fused cross-attention K|V cache
   };
@@ -143,8 +147,13 @@ class Unet : public Model {
   void run(Ctx& c, const void* x, int B, int h, int w, const float* t, const void* kv, int L, float* eps);
   Act resnet(Ctx& c, const ResW& r, Act& x0, Act* x1, const float* tproj, float eps);
   Act transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L);
+  // LayerNorm(x) -> projection g (g.A / lda / bias set here): folded into g's epilogue when ln_fold_ and the shape
+  // takes it (statistics only, written to `st`), else through the normalised copy `nbuf`
+  void ln_gemm(Ctx& c, GemmArgs& g, const void* x, int rows, int C, P lnw, P lnb, P u, P v, const float* bias,
+               void* nbuf, float2* st);
 
   int cin_pad_ = 8;
+  bool ln_fold_ = false;   // LayerNorm folded into the transformer projections (fixed at creation: the blob layout)
   int temb_dim_ = 1280;
   long temb_cols_ = 0, kv_cols_ = 0;
   std::vector<std::string> temb_names_w_, temb_names_b_, kv_names_;

@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x0,
 template <typename T, int MAXV, int RPW>
 __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long ldx, int rows, int C, float eps,
                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                 T* __restrict__ out, long ldo) {
+                                                 T* __restrict__ out, long ldo, float2* __restrict__ stats) {
   constexpr int VEC = 16 / (int)sizeof(T);
   const int lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
@@ -380,6 +380,10 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long l
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
     const float rstd = rsqrtf(q / C + eps);
+    if (stats) {   // statistics only (the folded projections' epilogue applies them)
+      if (lane == 0) stats[row] = make_float2(rstd, rstd * mean);
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
       const int v = lane + 64 * i;
@@ -388,7 +392,8 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long l
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
           const int c = v * VEC + e;
-          y[e] = fmaf((f[i][e] - mean) * rstd, gamma[c], beta[c]);   // (the form the fused epilogue shares)
+          y[e] = gamma ? fmaf((f[i][e] - mean) * rstd, gamma[c], beta[c])   // (the form the fused epilogue shares)
+                       : (f[i][e] - mean) * rstd;
         }
         *(uint4*)(out + (long)row * ldo + v * VEC) = Vec16<T>::pack(y);
       }
@@ -465,23 +470,24 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
 
 template <typename T>
 void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamma, const float* beta, void* out,
-          long ldo, hipStream_t s) {
+          long ldo, hipStream_t s, float2* stats = nullptr) {
   const int VEC = 16 / (int)sizeof(T);
   const int nv = C / VEC;
   dim3 block(256);
-  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::ln_kernel") : std::string(), 0.0, s);
+  ProfScope ps(prof_on() ? std::string(stats ? "irx::(anonymous namespace)::ln_kernel(stats)"
+                                              : "irx::(anonymous namespace)::ln_kernel") : std::string(), 0.0, s);
   // rows per wave: 4 while the row is <= 2 vectors per lane (fill the chip first: >= ~2048 blocks), else 2 / 1
   auto grid = [&](int rpw) { return dim3((rows + 4 * rpw - 1) / (4 * rpw)); };
   if (nv <= 64) {
-    if (rows >= 4 * 4 * 2048) ln_kernel<T, 1, 4><<<grid(4), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
-    else ln_kernel<T, 1, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
+    if (rows >= 4 * 4 * 2048) ln_kernel<T, 1, 4><<<grid(4), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
+    else ln_kernel<T, 1, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
   } else if (nv <= 128) {
-    if (rows >= 4 * 2 * 2048) ln_kernel<T, 2, 2><<<grid(2), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
-    else ln_kernel<T, 2, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
+    if (rows >= 4 * 2 * 2048) ln_kernel<T, 2, 2><<<grid(2), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
+    else ln_kernel<T, 2, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
   } else if (nv <= 256) {
-    ln_kernel<T, 4, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
+    ln_kernel<T, 4, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
   } else if (nv <= 512) {
-    ln_kernel<T, 8, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo);
+    ln_kernel<T, 8, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
   } else {
     throw Error("layer_norm: C too large");
   }
@@ -539,9 +545,19 @@ void layer_norm(int dtype, const void* x, long ldx, int rows, int C, float eps, 
                 const float* beta, void* out, long ldo, hipStream_t s) {
   const int vec = dtype == F32 ? 4 : 8;
   IRX_CHECK(C % vec == 0 && ldx % vec == 0 && ldo % vec == 0, "LayerNorm: rows must be 16-byte multiples");
+  IRX_CHECK((gamma == nullptr) == (beta == nullptr), "LayerNorm: gamma and beta both or neither");
   if (dtype == F32) ln_t<float>(x, ldx, rows, C, eps, gamma, beta, out, ldo, s);
   else if (dtype == F16) ln_t<f16_t>(x, ldx, rows, C, eps, gamma, beta, out, ldo, s);
   else ln_t<bf16_t>(x, ldx, rows, C, eps, gamma, beta, out, ldo, s);
+}
+
+void layer_norm_stats(int dtype, const void* x, long ldx, int rows, int C, float eps, float2* stats, hipStream_t s) {
+  const int vec = dtype == F32 ? 4 : 8;
+  IRX_CHECK(C % vec == 0 && ldx % vec == 0, "LayerNorm: rows must be 16-byte multiples");
+  IRX_CHECK(stats, "LayerNorm statistics: null output");
+  if (dtype == F32) ln_t<float>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 0, s, stats);
+  else if (dtype == F16) ln_t<f16_t>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 0, s, stats);
+  else ln_t<bf16_t>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 0, s, stats);
 }
 
 }  // namespace irx

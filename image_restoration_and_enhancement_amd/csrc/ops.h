@@ -54,6 +54,12 @@ struct GemmArgs {
   // gemm_emits_gn_parts) and per output channel, the (sum, sum of squares) of the stored values as double2 at
   // gn_part[(m / R) * N + n] (shifted fp32 sums per thread, fp64 merge: gn_stats3's arithmetic)
   double* gn_part = nullptr;
+  // LayerNorm of the A rows folded into the product (16-bit transformer projections, gemm_ln_foldable): B holds
+  // W * gamma (columns scaled), `bias` holds bias + W beta, and the epilogue forms
+  //   y[m][n] = ln_rs[m].x * acc[m][n] - ln_rs[m].y * ln_u[n] + bias[n]
+  // with ln_rs[m] = (rstd, rstd * mean) of row m of A (layer_norm_stats) and ln_u[n] = sum_k B[n][k]:
+  // exactly LN(x) W^T + bias, with no normalised copy of A written or read.
+  const float2* ln_rs = nullptr; const float* ln_u = nullptr;
   void* splitk_ws = nullptr; size_t splitk_ws_bytes = 0;   // caller workspace for split-K partials
   int dbg = 0;            // large-tile diagnostics (irx_set_option("gemm_dbg")): 1 skip epilogue, 2 skip MFMAs
 };
@@ -72,6 +78,8 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path
 size_t gemm_workspace_bytes(const GemmArgs& a);           // split-K partial buffer the call will use
 bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can apply the GEGLU epilogue
 bool gemm_gn_fusable(const GemmArgs& a);                  // conv can apply GemmArgs::gn_ab to its operand
+bool gemm_ln_foldable(const GemmArgs& a);                 // large-tile epilogue can apply GemmArgs::ln_rs / ln_u
+extern int g_ln_fold;      // 1: 16-bit UNets fold LayerNorm into the following projections (read at model creation)
 int gemm_emits_gn_parts(const GemmArgs& a);   // rows per GroupNorm partial this call's epilogue emits (0: none)
 extern int g_gn_parts;     // 1: producers emit GroupNorm partial sums, the stats pass is skipped (0: A/B)
 extern int g_gn_fuse;      // 1: GroupNorm(+SiLU) folded into the following halo conv where it fits (0: A/B)
@@ -103,8 +111,11 @@ void group_norm_parts(int dtype, const void* x0, const void* x1, int C0, int C1,
 // `ab` [N][C0 + C1] (float2), for a consumer that applies them itself (GemmArgs::gn_ab)
 void group_norm_stats(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
                       const float* gamma, const float* beta, float2* ab, void* ws, hipStream_t s);
+// gamma / beta may be null: no affine (y = (x - mean) * rstd), the form the folded projections' fallback uses
 void layer_norm(int dtype, const void* x, long ldx, int rows, int C, float eps, const float* gamma,
                 const float* beta, void* out, long ldo, hipStream_t s);
+// per-row (rstd, rstd * mean) only (GemmArgs::ln_rs): one read of x, the statistics of layer_norm exactly
+void layer_norm_stats(int dtype, const void* x, long ldx, int rows, int C, float eps, float2* stats, hipStream_t s);
 
 // ------------------------------------------------------------ attention
 // Multi-head attention, flash-style (online softmax, never materialises scores).

@@ -80,6 +80,7 @@ class ParamSpec:
     nbytes: int
     row_scale: float = 1.0
     scale_rows: int = 0
+    aux: str = ""
 
 
 def geglu64_order(n: int) -> torch.Tensor:
@@ -146,7 +147,8 @@ class NativeModel:
             L.call("irx_model_param_info", self.h, i, C.byref(info))
             out.append(ParamSpec(info.name.decode(), info.layout, info.dtype,
                                  tuple(int(info.shape[k]) for k in range(info.ndim)), int(info.offset),
-                                 int(info.bytes), float(info.row_scale), int(info.scale_rows)))
+                                 int(info.bytes), float(info.row_scale), int(info.scale_rows),
+                                 (info.aux or b"").decode()))
         return out
 
     def blob_bytes(self) -> int:
@@ -155,14 +157,40 @@ class NativeModel:
         return int(b.value)
 
     def pack(self, sd: Dict[str, torch.Tensor]) -> torch.Tensor:
-        """Host uint8 blob laid out per the native manifest (layout conversion, fusion, padding, cast)."""
+        """Host uint8 blob laid out per the native manifest (layout conversion, fusion, padding, cast; the
+        LayerNorm fold of IRX_LAYOUT_VEC_LN_U / _LN_V, include/irx.h)."""
         blob = torch.zeros(self.blob_bytes(), dtype=torch.uint8)
-        for p in self.manifest():
+        mats: Dict[str, Tuple[ParamSpec, torch.Tensor, torch.Tensor]] = {}   # spec -> (entry, W as packed, cast W')
+
+        def matrix(p: ParamSpec) -> torch.Tensor:      # converted, concatenated, row-scaled (fp32)
             parts = [_convert(sd[n], p.layout) for n in p.name.split("|")]
             t = parts[0] if len(parts) == 1 else torch.cat(parts, dim=0)
             if p.scale_rows:
                 t = t.clone()
                 t[:p.scale_rows] *= p.row_scale
+            return t
+
+        for p in self.manifest():
+            if p.layout == L.IRX_LAYOUT_VEC_LN_U:
+                _, _, wq = mats[p.name]
+                t = wq.double().sum(dim=1).float()
+            elif p.layout == L.IRX_LAYOUT_VEC_LN_V:
+                e, w, _ = mats[p.name]
+                beta_name, bias_spec = p.aux.split(";")
+                t = (w.double() @ sd[beta_name].double().reshape(-1)).float()
+                if bias_spec:
+                    vl = L.IRX_LAYOUT_VEC_GEGLU64 if e.layout == L.IRX_LAYOUT_MAT_GEGLU64 else L.IRX_LAYOUT_VEC
+                    t = t + torch.cat([_convert(sd[n], vl) for n in bias_spec.split("|")])
+            else:
+                t = matrix(p) if p.layout in (L.IRX_LAYOUT_MAT, L.IRX_LAYOUT_MAT_GEGLU64) else None
+                if t is None:
+                    parts = [_convert(sd[n], p.layout) for n in p.name.split("|")]
+                    t = parts[0] if len(parts) == 1 else torch.cat(parts, dim=0)
+                if p.aux:                                  # LayerNorm gamma folded into the columns
+                    w = t
+                    t = t * sd[p.aux].float().reshape(1, -1)
+                    wq = _pad_to(t, p.shape).to(TORCH_DT[p.dtype]).float()[:t.shape[0], :t.shape[1]]
+                    mats[p.name] = (p, w, wq)
             t = _pad_to(t, p.shape).to(TORCH_DT[p.dtype]).contiguous()
             if t.numel() * t.element_size() != p.nbytes:
                 raise ValueError(f"{p.name}: packed {t.numel() * t.element_size()} bytes, manifest {p.nbytes}")

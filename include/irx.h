@@ -39,6 +39,15 @@ extern "C" {
  * 64 gate rows) block pairs: packed row r <- source row (r/128)*64 + r%64 (+ N/2 if r%128 >= 64) */
 #define IRX_LAYOUT_MAT_GEGLU64 4
 #define IRX_LAYOUT_VEC_GEGLU64 5
+/* LayerNorm folded into the projection it feeds (16-bit UNets; diffusers BasicTransformerBlock norm1/2/3 ->
+ * attn1.to_q|k|v, attn2.to_q, ff.net.0.proj).  The matrix entry names its LN weight in `aux`: the packer scales
+ * its columns by gamma (after any re-ordering / row scaling, before the cast).  Two fp32 vectors follow it,
+ * named after the same matrix spec:
+ *   VEC_LN_U  u[n] = sum_k of the packed (cast) matrix row n
+ *   VEC_LN_V  v[n] = bias[n] + sum_k W[n][k] * beta[k]  (W re-ordered / row-scaled as packed, before gamma);
+ *             aux = "<beta name>;<bias spec or empty>" */
+#define IRX_LAYOUT_VEC_LN_U 6
+#define IRX_LAYOUT_VEC_LN_V 7
 
 typedef struct irx_model irx_model;
 
@@ -73,6 +82,7 @@ typedef struct {
    * softmax scale * log2(e) folded into to_q in the 16-bit engines (the kernels then take q pre-scaled) */
   float row_scale;
   int64_t scale_rows;
+  const char* aux;    /* IRX_LAYOUT_MAT*: column-scale vector name ("" = none); VEC_LN_V: "<beta>;<bias>" */
 } irx_param_info;
 
 const char* irx_last_error(void);

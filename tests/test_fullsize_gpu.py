@@ -8,7 +8,8 @@ Tolerances:
   * fp32 engine vs the CPU oracle: UNet / VAE relative max error 2e-4; end-to-end |decoded pixel diff| < 1e-3
     on the [0, 1] scale (the north star's fp32 bound) and <= 1 uint8 level;
   * bf16 engine: UNet / VAE encoder / VAE decoder relative L2 error < 4e-2 / 3e-2 / 5e-2; end-to-end row 0 of the batch vs the fp32
-    oracle: PSNR of the uint8 images >= 35 dB and relative L2 of the decoded [0, 1] pixels < 2e-2.
+    oracle: PSNR of the uint8 images >= 45 dB and relative L2 of the decoded [0, 1] pixels < 1e-2 (the full-length
+    runs are gated in tests/test_e2e_golden_gpu.py).
 """
 import functools
 import math
@@ -29,8 +30,8 @@ from tests import opref as O
 
 pytestmark = pytest.mark.gpu
 
-BF16_PSNR_MIN = 35.0
-BF16_REL_L2_MAX = 2e-2
+BF16_PSNR_MIN = 45.0      # (round 2: 35 dB; the full-length runs of test_e2e_golden_gpu.py measure 50-60 dB)
+BF16_REL_L2_MAX = 1e-2
 
 
 def _r(*shape, seed=0, scale=1.0):
@@ -219,6 +220,7 @@ def _check_bf16_batch(got, ref, n):
     a = got.decoded01[0].cpu().numpy()
     rel = float(np.linalg.norm(a - ref.decoded_float) / np.linalg.norm(ref.decoded_float))
     p = M.psnr(np.asarray(ref.image), got.images_u8[0].cpu().numpy())
+    print(f"\n16-bit row 0 vs oracle: PSNR {p:.2f} dB, rel L2 {rel:.3e}")
     assert rel < BF16_REL_L2_MAX and p >= BF16_PSNR_MIN, (rel, p)
     assert got.images_u8.shape[0] == n
 

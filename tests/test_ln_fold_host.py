@@ -1,0 +1,85 @@
+"""CPU test of the LayerNorm fold the 16-bit UNets pack (include/irx.h IRX_LAYOUT_VEC_LN_U / _LN_V; GemmArgs::ln_rs):
+for every folded projection, the packed (W * gamma, u, v) reproduce LN(x) W^T + b as
+    rstd * (x W'^T) - rstd * mean * u + v
+on random rows — the identity the GEMM epilogue applies (no GPU: manifest + packer only).  The fp32 engine packs
+no fold."""
+import numpy as np
+import pytest
+import torch
+
+from image_restoration_and_enhancement_amd import _lib as L
+from image_restoration_and_enhancement_amd import weights as W
+from image_restoration_and_enhancement_amd.configs import UNetConfig
+from image_restoration_and_enhancement_amd.engine import UNet, TORCH_DT
+
+
+def _small_cfg():
+    c = UNetConfig()
+    c.block_out_channels = [64, 128]
+    c.down_attn = [True, False]
+    c.up_attn = [False, True]
+    c.layers_per_block = 1
+    c.cross_attention_dim = 64
+    return c
+
+
+def _entries(m, blob):
+    out = {}
+    for p in m.manifest():
+        t = blob[p.offset:p.offset + p.nbytes].view(TORCH_DT[p.dtype]).float().reshape(p.shape)
+        out[(p.name, p.layout)] = (p, t)
+    return out
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_ln_fold_identity(dtype):
+    cfg = _small_cfg()
+    m = UNet(cfg, dtype, "cpu")
+    sd = W.random_state_dict("unet", cfg, 3)
+    e = _entries(m, m.pack(sd))
+    folded = [k for k, (p, _) in e.items() if k[1] in (L.IRX_LAYOUT_MAT, L.IRX_LAYOUT_MAT_GEGLU64) and p.aux]
+    assert len(folded) == 3 * 4          # (qkv, attn2.to_q, ff.net.0.proj) x 4 transformers (down, mid, 2 up)
+    g = torch.Generator().manual_seed(0)
+    for name, lay in folded:
+        p, wq = e[(name, lay)]
+        u = e[(name, L.IRX_LAYOUT_VEC_LN_U)][1]
+        pv, v = e[(name, L.IRX_LAYOUT_VEC_LN_V)]
+        C = wq.shape[1]
+        x = torch.randn(7, C, generator=g, dtype=torch.float64) * 3 + 1.5
+        mean, var = x.mean(1, keepdim=True), x.var(1, unbiased=False, keepdim=True)
+        rstd = 1 / torch.sqrt(var + 1e-5)
+        got = rstd * (x @ wq.double().T) - rstd * mean * u.double() + v.double()
+        # reference: LN with the diffusers weights, the unfused packing of W (re-order, row scale), + bias
+        gamma = sd[p.aux].double()
+        beta_name, bias_spec = pv.aux.split(";")
+        ln = (x - mean) * rstd * gamma + sd[beta_name].double()
+        parts = [sd[n].double().reshape(sd[n].shape[0], -1) for n in name.split("|")]
+        w = torch.cat(parts)
+        if lay == L.IRX_LAYOUT_MAT_GEGLU64:
+            from image_restoration_and_enhancement_amd.engine import geglu64_order
+            w = w[geglu64_order(w.shape[0])]
+        if p.scale_rows:
+            w[:p.scale_rows] *= p.row_scale
+        ref = ln @ w.T
+        if bias_spec:
+            b = torch.cat([sd[n].double().reshape(-1) for n in bias_spec.split("|")])
+            if lay == L.IRX_LAYOUT_MAT_GEGLU64:
+                from image_restoration_and_enhancement_amd.engine import geglu64_order
+                b = b[geglu64_order(b.numel())]
+            ref = ref + b
+        tol = 2e-2 if dtype == "bf16" else 3e-3      # the 16-bit rounding of W * gamma
+        assert float((got - ref).norm() / ref.norm()) < tol, name
+
+
+def test_fp32_engine_packs_no_fold():
+    m = UNet(_small_cfg(), "fp32", "cpu")
+    assert not any(p.aux or p.layout in (L.IRX_LAYOUT_VEC_LN_U, L.IRX_LAYOUT_VEC_LN_V) for p in m.manifest())
+
+
+def test_ln_fold_option_off_packs_plain(monkeypatch):
+    L.call("irx_set_option", b"ln_fold", 0)
+    try:
+        m = UNet(_small_cfg(), "bf16", "cpu")
+        assert not any(p.aux for p in m.manifest())
+    finally:
+        L.call("irx_set_option", b"ln_fold", 1)
