@@ -142,17 +142,33 @@ def build_engine(cfg, dtype, device, rank):
     return eng, sds, how
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (scripts/pmc_traffic.py;
-    FETCH_SIZE x2 + WRITE_SIZE per the gfx950 note), or None when no pass for this kernel is committed."""
+def _norm_kernel(name: str) -> str:
+    return name.replace("(anonymous namespace)::", "").replace("void ", "").replace(" ", "")
+
+
+def pmc_counters(kernel: str) -> dict:
+    """Committed rocprofv3 PMC figures for `kernel` (scripts/pmc_top.py -> profiles/*pmc_top*.json, newest
+    first; else the per-kernel FETCH / WRITE passes of scripts/pmc_traffic.py): HBM bytes per launch
+    (FETCH_SIZE x2 + WRITE_SIZE per the gfx950 note), the HBM GB/s of that pass and the MFMA busy fraction
+    (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE / 8 x 1024 SIMDs).  Empty when no pass for it is committed."""
+    want = _norm_kernel(kernel)
+    for f in sorted(ROOT.glob("profiles/*pmc_top*.json"), reverse=True):
+        try:
+            d = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        for k in d.get("kernels", []):
+            if _norm_kernel(k["kernel"]) == want:
+                return {"traffic": k["hbm_bytes_per_launch"], "hbm_gbps": k["hbm_gbps"],
+                        "mfma_busy": k["mfma_busy"], "pmc_source": f.name}
     for f in sorted(ROOT.glob("profiles/*pmc_traffic*.json"), reverse=True):
         try:
             d = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
         if d.get("kernel") and kernel.endswith("::" + d["kernel"]):
-            return round(d["bytes_per_launch"])
-    return None
+            return {"traffic": round(d["bytes_per_launch"]), "pmc_source": f.name}
+    return {}
 
 
 def usable_cpus() -> int:
@@ -332,8 +348,11 @@ def main():
         name, cnt, ms, fl = next(p for p in prof if p[3] > 0)   # dominant MFMA kernel
         peak = PEAK_TFLOPS[dtype]
         ach = fl / (ms * 1e-3) / 1e12
+        pmc = pmc_counters(name)
         roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(ach / peak, 4), "traffic": pmc_traffic(name), "kernel": name,
+                    "frac": round(ach / peak, 4), "traffic": pmc.get("traffic"),
+                    "mfma_busy": pmc.get("mfma_busy"), "hbm_gbps": pmc.get("hbm_gbps"),
+                    "hbm_peak_gbps": 8000.0, "pmc_source": pmc.get("pmc_source"), "kernel": name,
                     "launches": cnt, "avg_launch_us": round(ms * 1e3 / cnt, 2),
                     "flops_per_launch": fl / cnt,
                     "all_mfma_kernels_tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 2),
