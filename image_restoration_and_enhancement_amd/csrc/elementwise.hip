@@ -26,7 +26,7 @@ __global__ void geglu_kernel(const T* __restrict__ p, long ldp, int M, int F, T*
   Vec16<T>::unpack(*(const uint4*)(p + (long)m * ldp + hc), h);
   Vec16<T>::unpack(*(const uint4*)(p + (long)m * ldp + gc), g);
 #pragma unroll
-  for (int e = 0; e < VEC; ++e) h[e] = h[e] * gelu_erf(g[e]);
+  for (int e = 0; e < VEC; ++e) h[e] = h[e] * (sizeof(T) == 4 ? gelu_erf(g[e]) : gelu_erf16(g[e]));
   *(uint4*)(o + (long)m * ldo + v * VEC) = Vec16<T>::pack(h);
 }
 

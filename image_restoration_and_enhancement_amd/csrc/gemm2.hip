@@ -20,6 +20,7 @@
 #include <map>
 #include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "ops.h"
 #include "profile.h"
@@ -46,6 +47,11 @@ struct Split {
   int Mp = 0, Np = 0;
   unsigned* cnt = nullptr;   // this stream's arrival tickets (in-kernel mode)
 };
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
 
 // Wait until at most n of this wave's vector-memory operations (here: LDS-DMA pieces) are outstanding.
 __device__ __forceinline__ void wait_vm(int n) {
@@ -306,29 +312,43 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         glds16_asm(src, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
       }
     };
+    // ---- fragment addressing, hoisted out of the K loop.  With the 9 taps of a slab unrolled, the tap (ky, kx)
+    //      and the B stage (kt % 3 == t % 3: splits start at whole slabs) are compile-time, so every fragment
+    //      address is a per-lane offset (6 A variants: kx x sub-step; 2 B variants) + a wave-uniform base + an
+    //      immediate.  The A swizzle of halo row hp is hp & 7 = (frow + kx - 1) & 7 (W and i * 16 are
+    //      multiples of 8).
+    int aoff[3][KSUB], boff[KSUB];
+#pragma unroll
+    for (int ss = 0; ss < KSUB; ++ss) {
+      const int ck = ss * 4 + fgrp;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) aoff[kx][ss] = frow * CPR + (ck ^ ((frow + kx - 1) & 7));
+      boff[ss] = frow * CPR + (ck ^ (frow & 7));
+    }
+    const int awave = wm * TM * 16 * CPR, bwave = wn * TN * 16 * CPR, rowW = W * CPR;
+    bool zl[TM], zr[TM];   // fragment rows at the image's left / right edge: taps kx = 0 / 2 read the zero row
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rx = (wm * TM * 16 + i * 16 + frow) & (W - 1);
+      zl[i] = rx == 0;
+      zr[i] = rx == W - 1;
+    }
     uint4 fa[KSUB][TM], fb[KSUB][TN];
-    auto readF = [&](int kt) {   // this wave's fragments of step kt (both 32-deep sub-steps)
-      const int c = kt / 9, t = kt - 9 * c;
-      const int ky = t / 3, kx = t - 3 * ky;
-      const int shift = ky * W + kx - 1;
-      const uint4* Hs = Hb + (c & 1) * HB_U4;
-      const uint4* Bs = Bsm + (kt % S) * BN * CPR;
+    auto readF = [&](auto tc, const uint4* Hs) {   // this wave's fragments of tap t (both 32-deep sub-steps)
+      constexpr int t = decltype(tc)::value, ky = t / 3, kx = t % 3, st = t % S;
+      const uint4* Bs = Bsm + st * BN * CPR + bwave;
+      const uint4* Hrow = Hs + awave + ky * rowW + (kx - 1) * CPR;
 #pragma unroll
       for (int ss = 0; ss < KSUB; ++ss) {
-        const int ck = ss * 4 + fgrp;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const int r = wm * TM * 16 + i * 16 + frow;
-          const int rx = r & (W - 1);
-          const int hp = r + shift;
-          const bool zero = (kx == 0 && rx == 0) || (kx == 2 && rx == W - 1);
-          fa[ss][i] = zero ? zrow[ck] : Hs[hp * CPR + (ck ^ swz(hp))];
+          const uint4* src = Hrow + aoff[kx][ss] + i * 16 * CPR;
+          if constexpr (kx == 0) src = zl[i] ? zrow + ss * 4 + fgrp : src;
+          if constexpr (kx == 2) src = zr[i] ? zrow + ss * 4 + fgrp : src;
+          fa[ss][i] = *src;
         }
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int r = wn * TN * 16 + j * 16 + frow;
-          fb[ss][j] = Bs[r * CPR + (ck ^ swz(r))];
-        }
+        for (int j = 0; j < TN; ++j) fb[ss][j] = Bs[boff[ss] + j * 16 * CPR];
       }
     };
     auto mma = [&]() {
@@ -357,23 +377,31 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     // barrier}, group 1 one phase behind group 0 (one extra barrier in front, group 0 one extra at the end),
     // so each interval between barriers pairs one group's MFMAs with the other group's loads
     if (g1) barrier();
-    for (int kt = kt0; kt < nk; ++kt) {
-      const int c = kt / 9, t = kt - 9 * c;
-      // ---- load phase
-      if (g1) {
-        if (kt + 2 < nk) issueB(kt + 2);
-      } else if (kt > kt0) {   // the halo part scheduled after step kt - 1
-        const int cp = (kt - 1) / 9, tp = kt - 1 - 9 * cp;
-        if (tp == 8 && cp + 2 < cend) issueH(cp + 2, 0, HPP);
-        else if (tp < HPARTS - 1 && cp > c0 && cp + 1 < cend) issueH(cp + 1, (tp + 1) * HPP, (tp + 2) * HPP);
-      }
-      readF(kt);
-      if (g1 && kt + 1 < nk) wait_vm(kt + 2 < nk ? BPG : 0);   // B(kt + 1) landed (group 0 reads it next)
-      barrier();
-      // ---- compute phase
-      mma();
-      if (!g1 && t == 8 && c + 1 < cend) wait_vm(0);              // the next slab's halo landed
-      barrier();
+    for (int c = c0; c < cend; ++c) {
+      const uint4* Hs = Hb + (c & 1) * HB_U4;
+      const bool last = c + 1 == cend;
+      const bool halo_next = c > c0 && !last;            // group 0 streams slab c + 1's halo at taps 0..5
+      static_for(std::make_integer_sequence<int, 9>{}, [&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        const int kt = 9 * c + t;
+        // ---- load phase
+        if (g1) {
+          if (!(last && t >= 7)) issueB(kt + 2);
+        } else if (t < HPARTS && halo_next) {
+          issueH(c + 1, t * HPP, (t + 1) * HPP);
+        }
+        readF(tc, Hs);
+        if (g1 && !(last && t == 8)) {                   // B(kt + 1) landed (group 0 reads it next)
+          if (last && t == 7) wait_vm(0);
+          else wait_vm(BPG);
+        }
+        barrier();
+        // ---- compute phase
+        mma();
+        if (!g1 && t == 8 && !last) wait_vm(0);          // the next slab's halo landed
+        barrier();
+        (void)kt;
+      });
     }
     if (!g1) barrier();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -686,7 +714,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           Vec16<T>::unpack(*(const uint4*)(tileS + row * BN + ((hc ^ (row & 7)) << 3)), h);
           Vec16<T>::unpack(*(const uint4*)(tileS + row * BN + (((hc + 8) ^ (row & 7)) << 3)), gt);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) h[e] = h[e] * gelu_erf(gt[e]);
+          for (int e = 0; e < 8; ++e) h[e] = h[e] * gelu_erf16(gt[e]);
           *(uint4*)(Cp + (long)m * a.ldc + n0 / 2 + oc * 8) = Vec16<T>::pack(h);
         }
         return;
