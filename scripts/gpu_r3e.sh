@@ -17,3 +17,6 @@ timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no
 cat $O/bench_nofold.json
 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline > $O/bench2.json 2> $O/bench2.err || { tail $O/bench2.err; exit 1; }
 cat $O/bench2.json
+timeout -k 10 900 python3 scripts/pmc_top.py run --dir $O/top --timeout 280 || exit 1
+python3 scripts/pmc_top.py summarize --dir $O/top --out $O/pmc_top.json --top 12
+rm -rf $O/top/*/*.db

@@ -44,12 +44,13 @@ XCDS = 8
 def short(name: str) -> str:
     name = re.sub(r"\(anonymous namespace\)::", "", name)
     name = re.sub(r"^void ", "", name)
-    return name[:160]
+    return name.split("(")[0][:160]          # drop the argument list: the bench profiler's spelling
 
 
 def run(d: Path, bench_args: str, timeout: int) -> None:
     d.mkdir(parents=True, exist_ok=True)
-    env = dict(os.environ, TMPDIR="/tmp")
+    # eager launches: counter collection over replayed HIP graphs segfaulted the profiled process (r3d)
+    env = dict(os.environ, TMPDIR="/tmp", IRX_GRAPHS="0")
     for tag, counters in PASSES.items():
         cmd = (["timeout", "-s", "KILL", str(timeout), "rocprofv3", "--pmc", *counters.split(),
                 "--output-format", "csv", "-d", str(d / tag), "-o", tag, "--", sys.executable, "bench.py"]
