@@ -37,6 +37,7 @@ PASSES = {
     "fetch": "FETCH_SIZE",
     "write": "WRITE_SIZE",
 }
+KERNELS = "gemm2_kernel|attn3_kernel|attnw_kernel|gemm_kernel|attn_kernel"
 SIMDS = 1024
 XCDS = 8
 
@@ -52,7 +53,10 @@ def run(d: Path, bench_args: str, timeout: int) -> None:
     # eager launches: counter collection over replayed HIP graphs segfaulted the profiled process (r3d)
     env = dict(os.environ, TMPDIR="/tmp", IRX_GRAPHS="0")
     for tag, counters in PASSES.items():
+        # MFMA kernels only: collecting over every kernel of the bench segfaulted the profiled process inside
+        # a GroupNorm launch (r3e), whatever the graph setting
         cmd = (["timeout", "-s", "KILL", str(timeout), "rocprofv3", "--pmc", *counters.split(),
+                "--kernel-include-regex", KERNELS,
                 "--output-format", "csv", "-d", str(d / tag), "-o", tag, "--", sys.executable, "bench.py"]
                + bench_args.split())
         print("+", " ".join(cmd), flush=True)
