@@ -68,6 +68,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gn_parts") g_gn_parts = value;
   else if (n == "halo_split") g_halo_split = value;
   else if (n == "halo_pipe") g_halo_pipe = value;
+  else if (n == "gemm_pp") g_gemm_pp = value;
   else if (n == "ln_fold") g_ln_fold = value;
   else if (n == "vae_attn_rows") g_vae_attn_rows = value;
   else if (n == "vae_flash") g_vae_flash = value;

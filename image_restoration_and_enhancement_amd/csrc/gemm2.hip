@@ -85,7 +85,7 @@ __device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds_addr) {
 constexpr int kHaloWMax = 64;    // widest image row a halo tile takes (LDS: 2 x (BM + 2W) x 2BK B)
 
 template <typename T, int BM, int BN, int WM, int WN, int BK, int S, bool CONV, bool OUTF32, bool RESIZE,
-          int HALO = 0>
+          int HALO = 0, bool PP = false>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kernel(GemmArgs a, Split sp) {
   constexpr int NW = WM * WN, NT = NW * 64;   // 8 waves (1 block/CU) or 4 waves (2 blocks/CU)
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
@@ -100,7 +100,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   static_assert(!HALO || (CONV && !RESIZE && S >= 2 && S <= 8 && NW == 8), "halo tiles: 3x3 conv");
   constexpr int HB_U4 = (BM + 2 * kHaloWMax) * CPR;   // one halo slab buffer (uint4)
   constexpr int RING = HALO ? 2 * HB_U4 + S * BN * CPR + CPR + 64 : S * STAGE;
-  constexpr int SMEM = (RING > BM * BN / 8 ? RING : BM * BN / 8) + (!HALO && NINST % NW ? 64 : 0);
+  // (+ a scratch KiB for the surplus DMA pieces, inside the epilogue's staging area when the ring is smaller)
+  constexpr int RINGX = RING + (!HALO && NINST % NW ? 64 : 0);
+  constexpr int SMEM = RINGX > BM * BN / 8 ? RINGX : BM * BN / 8;
   static_assert(SMEM * 16 <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) uint4 smem[SMEM];
 
@@ -550,6 +552,75 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  } else if constexpr (PP) {
+    // ---- ping-pong main loop (the dense GEMM / im2col conv counterpart of the HALO == 2 schedule): the waves
+    //      w and w + 4 sharing a SIMD alternate between a load phase (LDS-DMA of step kt + 2, this wave's
+    //      fragment reads of step kt) and a compute phase (step kt's MFMAs), group 1 one phase behind group 0,
+    //      so every interval between barriers pairs one wave's MFMAs with its partner's loads.  S = 3 stages:
+    //      step kt + 2 goes into the stage of step kt - 1, whose fragments every wave read before the barrier
+    //      that ended its own load phase of kt - 1 (lgkmcnt(0) in `barrier`).  Each wave issues its IPW pieces
+    //      of every step; group 1 waits for its pieces of step kt + 1 at the end of its load phase of kt,
+    //      group 0 at the end of its compute phase of kt — both right before the barrier after which group 0
+    //      reads step kt + 1.
+    static_assert(S == 3 && NW == 8, "ping-pong: 3 stages, 8 waves");
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const bool g1 = wv >= NW / 2;
+    uint4 fa[KSUB][TM], fb[KSUB][TN];
+    auto readF = [&](int st) {
+      const uint4* As = smem + st * STAGE;
+      const uint4* Bs = As + BM * CPR;
+#pragma unroll
+      for (int s = 0; s < KSUB; ++s) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * TM * 16 + i * 16 + frow;
+          fa[s][i] = As[r * CPR + ((s * 4 + fgrp) ^ swz(r))];
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * TN * 16 + j * 16 + frow;
+          fb[s][j] = Bs[r * CPR + ((s * 4 + fgrp) ^ swz(r + BM))];
+        }
+      }
+    };
+    auto mma = [&]() {
+      if (a.dbg & 2) return;
+#pragma unroll
+      for (int s = 0; s < KSUB; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[s][i], fb[s][j], acc[i][j]);
+    };
+    auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    if (kt0 < kt1) issue(kt0, 0);
+    if (kt0 + 1 < kt1) issue(kt0 + 1, 1);
+    wait_vm(kt0 + 1 < kt1 ? IPW : 0);
+    barrier();
+    if (g1) barrier();
+    int st = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int st2 = st == 0 ? 2 : st - 1;              // the stage of step kt - 1 == that of kt + 2
+      // ---- load phase
+      if (kt + 2 < kt1) issue(kt + 2, st2);
+      readF(st);
+      if (g1 && kt + 1 < kt1) {
+        if (kt + 2 < kt1) wait_vm(IPW);
+        else wait_vm(0);
+      }
+      barrier();
+      // ---- compute phase
+      mma();
+      if (!g1 && kt + 1 < kt1) {
+        if (kt + 2 < kt1) wait_vm(IPW);
+        else wait_vm(0);
+      }
+      barrier();
+      st = st == 2 ? 0 : st + 1;
+    }
+    if (!g1) barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   } else if constexpr (S == 2) {
     if (kt0 < kt1) issue(kt0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -916,7 +987,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
   }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int BK, int S, int HALO>
+template <typename T, int BM, int BN, int WM, int WN, int BK, int S, int HALO, bool PP>
 void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, a.batch * sp.splits), block(WM * WN * 64);
@@ -927,17 +998,17 @@ void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
     nm = std::string("irx::(anonymous namespace)::gemm2_kernel<") + tn + ", " + std::to_string(BM) + ", " +
          std::to_string(BN) + ", " + std::to_string(WM) + ", " + std::to_string(WN) + ", " + std::to_string(BK) + ", " +
          std::to_string(S) + ", " + (a.conv ? "true" : "false") + ", " + (a.out_f32 ? "true" : "false") + ", " +
-         (rs ? "true" : "false") + ", " + std::to_string(HALO) + ">";
+         (rs ? "true" : "false") + ", " + std::to_string(HALO) + ", " + (PP ? "true" : "false") + ">";
   {
     ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
     if constexpr (HALO != 0) {
       gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false, HALO><<<grid, block, 0, s>>>(a, sp);
     } else if (a.conv) {   // (fp32-output convs never take this path: see eligible())
-      if (rs) gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, true><<<grid, block, 0, s>>>(a, sp);
-      else gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false><<<grid, block, 0, s>>>(a, sp);
+      if (rs) gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, true, 0, PP><<<grid, block, 0, s>>>(a, sp);
+      else gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false, 0, PP><<<grid, block, 0, s>>>(a, sp);
     } else {
-      if (a.out_f32) gemm2_kernel<T, BM, BN, WM, WN, BK, S, false, true, false><<<grid, block, 0, s>>>(a, sp);
-      else gemm2_kernel<T, BM, BN, WM, WN, BK, S, false, false, false><<<grid, block, 0, s>>>(a, sp);
+      if (a.out_f32) gemm2_kernel<T, BM, BN, WM, WN, BK, S, false, true, false, 0, PP><<<grid, block, 0, s>>>(a, sp);
+      else gemm2_kernel<T, BM, BN, WM, WN, BK, S, false, false, false, 0, PP><<<grid, block, 0, s>>>(a, sp);
     }
     IRX_LAUNCH_CHECK();
   }
@@ -954,10 +1025,10 @@ void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int S, int HALO = 0>
+template <int BM, int BN, int WM, int WN, int BK, int S, int HALO = 0, bool PP = false>
 void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
-  if (a.dtype == F16) launch2_t<f16_t, BM, BN, WM, WN, BK, S, HALO>(a, sp, s);
-  else launch2_t<bf16_t, BM, BN, WM, WN, BK, S, HALO>(a, sp, s);
+  if (a.dtype == F16) launch2_t<f16_t, BM, BN, WM, WN, BK, S, HALO, PP>(a, sp, s);
+  else launch2_t<bf16_t, BM, BN, WM, WN, BK, S, HALO, PP>(a, sp, s);
 }
 
 // ------------------------------------------------------------------ tile / split policy
@@ -969,7 +1040,7 @@ struct Choice {
                         // overlaps the other's MFMA loop)
 };
 
-int step_k() { return g_gemm_deep == 1 ? 32 : 64; }   // K depth of one pipeline stage
+int step_k() { return g_gemm_deep == 1 ? 32 : 64; }   // K depth of one pipeline stage (eligibility granule)
 
 // rows (M x batch) the policy plans for: image-indexed GEMMs at kCanonImages images (batch invariance)
 long canon_rows(const GemmArgs& a) {
@@ -1157,6 +1228,7 @@ size_t gemm_workspace_bytes(const GemmArgs& a) {
 // reduction) when two splits do, 0 = the halo path does not take the shape.
 int g_halo_split = 1;   // irx_set_option("halo_split", 0): no K-split halo tiles (A/B)
 int g_halo_pipe = 1;    // irx_set_option("halo_pipe", 0): the round-2 halo main loop (A/B)
+int g_gemm_pp = 1;      // irx_set_option("gemm_pp", 0): the round-2 two-stage main loop for dense GEMMs / im2col convs
 
 int halo_splits(const GemmArgs& a, long tiles) {
   if (tiles >= kCUs || g_conv_halo >= 2) return 1;
@@ -1238,6 +1310,18 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   if (c.small) {
     if (c.BN == 160) launch2<128, 160, 2, 2, 64, 2>(b, sp, s);
     else launch2<128, 128, 2, 2, 64, 2>(b, sp, s);
+  } else if (g_gemm_pp && g_gemm_deep == 0) {   // ping-pong schedule: 3 stages (BK 32 where BK 64 would not fit)
+    const int key = c.BM * 1000 + c.BN;
+    if (key == 256320 || key == 256256 || key == 128320) sp.per *= 2;   // K steps of 32
+    switch (key) {
+      case 256320: launch2<256, 320, 2, 4, 32, 3, 0, true>(b, sp, s); break;
+      case 256256: launch2<256, 256, 2, 4, 32, 3, 0, true>(b, sp, s); break;
+      case 128320: launch2<128, 320, 2, 4, 32, 3, 0, true>(b, sp, s); break;
+      case 256128: launch2<256, 128, 4, 2, 64, 3, 0, true>(b, sp, s); break;
+      case 128256: launch2<128, 256, 2, 4, 64, 3, 0, true>(b, sp, s); break;
+      case 128128: launch2<128, 128, 2, 4, 64, 3, 0, true>(b, sp, s); break;
+      default: return false;
+    }
   } else if (g_gemm_deep == 2) {   // BK 64; a third (fourth) stage wherever it fits in 160 KiB
     switch (c.BM * 1000 + c.BN) {
       case 256256: launch2<256, 256, 2, 4, 64, 2>(b, sp, s); break;

@@ -496,6 +496,51 @@ def test_conv_halo_pipelined_bit_exact(device, case, dt):
         L.call("irx_set_option", b"conv_halo", 1)
 
 
+@pytest.mark.parametrize("M,N,K,res,conv", [
+    (65536, 320, 320, True, None),        # K = 320 projections (256x320 tiles, BK 32)
+    (16384, 640, 640, True, None),        # 32x32 level (128x320 / split-K)
+    (4096, 1280, 1280, False, None),      # 16x16 level (128x128 tiles, BK 64, split-K)
+    (1000, 256, 512, False, None),        # ragged M
+    (65536, 1280, 320, False, "geglu"),   # GEGLU epilogue (256x256, BK 32)
+    (0, 640, 0, False, (16, 16, 16, 1280, 640)),   # im2col conv: 16x16 level, 1280 -> 640
+    (0, 320, 0, False, (8, 32, 32, 640, 320)),     # im2col conv: upsample-free 32x32, 640 -> 320 (1x1 shortcut)
+])
+@pytest.mark.parametrize("dt", DT16)
+def test_gemm_pingpong_bit_exact(device, M, N, K, res, conv, dt):
+    """The ping-pong main loop (option gemm_pp, default) issues every accumulator's MFMAs in the round-2 order
+    (32-deep K sub-steps, ascending; the same split-K boundaries): outputs identical bit for bit."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    from image_restoration_and_enhancement_amd.engine import geglu64_order
+    outs = []
+    try:
+        for pp in (0, 1):
+            L.call("irx_set_option", b"gemm_pp", pp)
+            if conv == "geglu":
+                C = K
+                A = _dev(_r(M, C, seed=300), dt, device)
+                W = _r(8 * C, C, seed=301, scale=1 / math.sqrt(C))[geglu64_order(8 * C)]
+                b = _r(8 * C, seed=302)
+                out = torch.empty(M, 4 * C, dtype=dt, device=device)
+                L.call("irx_op_gemm_geglu", O.S(), O.DT[dt], M, 8 * C, C, O.P(A), O.P(_dev(W, dt, device)),
+                       O.P(b.to(device).contiguous()), O.P(out))
+                outs.append(out)
+            elif conv is not None:
+                n, h, w, ci, co = conv
+                x = _dev(_r(n, h, w, ci, seed=303), dt, device)
+                k = 3 if h <= 16 else 1
+                wt = _r(co, ci, k, k, seed=304, scale=1 / math.sqrt(ci * k * k))
+                outs.append(O.conv2d(x, wt.to(dt).float(), _r(co, seed=305), pad=(k // 2, k // 2)))
+            else:
+                A = _dev(_r(M, K, seed=306), dt, device)
+                Bw = _dev(_r(N, K, seed=307, scale=1 / math.sqrt(K)), dt, device)
+                r = _dev(_r(M, N, seed=308), dt, device) if res else None
+                outs.append(O.gemm(A, Bw, bias=_r(N, seed=309).to(device).contiguous(), residual=r))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1])
+    finally:
+        L.call("irx_set_option", b"gemm_pp", 1)
+
+
 @pytest.mark.parametrize("B,L", [(2, 256), (1, 333), (2, 1024), (1, 77)])
 @pytest.mark.parametrize("dt", DT16)
 def test_attention_d512_flash(device, dt, B, L):
