@@ -1228,7 +1228,10 @@ size_t gemm_workspace_bytes(const GemmArgs& a) {
 // reduction) when two splits do, 0 = the halo path does not take the shape.
 int g_halo_split = 1;   // irx_set_option("halo_split", 0): no K-split halo tiles (A/B)
 int g_halo_pipe = 1;    // irx_set_option("halo_pipe", 0): the round-2 halo main loop (A/B)
-int g_gemm_pp = 1;      // irx_set_option("gemm_pp", 0): the round-2 two-stage main loop for dense GEMMs / im2col convs
+// irx_set_option("gemm_pp", 1): ping-pong main loop for dense GEMMs / im2col convs.  Off: measured slower at every
+// UNet / VAE shape (bench 553.8 vs 515.7 ms/step, the VAE 512x512 convs 1.9x; profiles/r03_kbench_*_pp.txt) — the
+// halo conv's gain came with its unrolled-tap addressing, which these loops do not need
+int g_gemm_pp = 0;
 
 int halo_splits(const GemmArgs& a, long tiles) {
   if (tiles >= kCUs || g_conv_halo >= 2) return 1;

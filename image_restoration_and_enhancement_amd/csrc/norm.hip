@@ -7,6 +7,8 @@
 // kernel folds them into mean/rstd.  Pass 2 folds gamma/beta into one per-channel scale/shift, and writes
 // y = x*a + b (optionally SiLU) with 16-byte vector stores.  Up-block inputs are a channel
 // concat of two tensors; groups may straddle the seam, so both passes read the two sources.
+#include <type_traits>
+
 #include "ops.h"
 #include "profile.h"
 
@@ -333,7 +335,8 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x0,
 
 // LayerNorm: one wave per row, row held in registers, two-pass mean/var in fp32.  RPW rows per wave with all
 // of their 16-byte loads issued before the first row's reductions (more bytes in flight per wave).
-template <typename T, int MAXV, int RPW>
+// MODE 0: y = ((x - mean) * rstd) * gamma + beta; 1: no affine; 2: statistics only (rstd, rstd * mean) per row
+template <typename T, int MAXV, int RPW, int MODE>
 __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long ldx, int rows, int C, float eps,
                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
                                                  T* __restrict__ out, long ldo, float2* __restrict__ stats) {
@@ -380,7 +383,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long l
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
     const float rstd = rsqrtf(q / C + eps);
-    if (stats) {   // statistics only (the folded projections' epilogue applies them)
+    if constexpr (MODE == 2) {   // statistics only (the folded projections' epilogue applies them)
       if (lane == 0) stats[row] = make_float2(rstd, rstd * mean);
       continue;
     }
@@ -392,8 +395,8 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long l
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
           const int c = v * VEC + e;
-          y[e] = gamma ? fmaf((f[i][e] - mean) * rstd, gamma[c], beta[c])   // (the form the fused epilogue shares)
-                       : (f[i][e] - mean) * rstd;
+          if constexpr (MODE == 0) y[e] = fmaf((f[i][e] - mean) * rstd, gamma[c], beta[c]);
+          else y[e] = (f[i][e] - mean) * rstd;
         }
         *(uint4*)(out + (long)row * ldo + v * VEC) = Vec16<T>::pack(y);
       }
@@ -478,19 +481,25 @@ void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamm
                                               : "irx::(anonymous namespace)::ln_kernel") : std::string(), 0.0, s);
   // rows per wave: 4 while the row is <= 2 vectors per lane (fill the chip first: >= ~2048 blocks), else 2 / 1
   auto grid = [&](int rpw) { return dim3((rows + 4 * rpw - 1) / (4 * rpw)); };
-  if (nv <= 64) {
-    if (rows >= 4 * 4 * 2048) ln_kernel<T, 1, 4><<<grid(4), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
-    else ln_kernel<T, 1, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
-  } else if (nv <= 128) {
-    if (rows >= 4 * 2 * 2048) ln_kernel<T, 2, 2><<<grid(2), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
-    else ln_kernel<T, 2, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
-  } else if (nv <= 256) {
-    ln_kernel<T, 4, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
-  } else if (nv <= 512) {
-    ln_kernel<T, 8, 1><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
-  } else {
-    throw Error("layer_norm: C too large");
-  }
+  auto launch = [&](auto mode) {
+    constexpr int MO = decltype(mode)::value;
+    if (nv <= 64) {
+      if (rows >= 4 * 4 * 2048) ln_kernel<T, 1, 4, MO><<<grid(4), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
+      else ln_kernel<T, 1, 1, MO><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
+    } else if (nv <= 128) {
+      if (rows >= 4 * 2 * 2048) ln_kernel<T, 2, 2, MO><<<grid(2), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
+      else ln_kernel<T, 2, 1, MO><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
+    } else if (nv <= 256) {
+      ln_kernel<T, 4, 1, MO><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
+    } else if (nv <= 512) {
+      ln_kernel<T, 8, 1, MO><<<grid(1), block, 0, s>>>((const T*)x, ldx, rows, C, eps, gamma, beta, (T*)out, ldo, stats);
+    } else {
+      throw Error("layer_norm: C too large");
+    }
+  };
+  if (stats) launch(std::integral_constant<int, 2>{});
+  else if (gamma) launch(std::integral_constant<int, 0>{});
+  else launch(std::integral_constant<int, 1>{});
   IRX_LAUNCH_CHECK();
 }
 

@@ -97,7 +97,7 @@ extern bool g_splitk_inkernel;
 extern bool g_tile_256x320;
 extern int g_gemm_force;
 extern int g_conv_halo;      // 3x3 convs on whole-row tiles: one LDS halo per 32-channel slab for all 9 taps
-extern int g_gemm_pp;        // 1: ping-pong main loop (wave pairs alternate MFMA / load phases) for dense GEMMs
+extern int g_gemm_pp;        // 1: ping-pong main loop for dense GEMMs (off: measured slower, see gemm2.hip)
 extern int g_halo_pipe;      // 1: software-pipelined halo main loop (fragments read one sub-step ahead)
 extern int g_halo_split;     // halo convs whose tiles alone do not fill the chip take two K splits
 extern bool g_gn_v2;       // GroupNorm stats v3 (slabbed grid + finalize kernel); 0 = v1 (A/B)

@@ -76,7 +76,7 @@ def main():
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
     base = {"large_tiles": 1, "gemm_deep": 0, "gemm_small": 0, "tile_256x320": 1, "splitk_inkernel": 1, "halo_pipe": 1,
-            "gemm_pp": 1}
+            "gemm_pp": 0}
     allv = {"s2": {}, "ring64": {"gemm_deep": 2}, "ring32": {"gemm_deep": 1}, "small": {"gemm_small": 1}, "4wave": {"large_tiles": 0},
             "no320": {"tile_256x320": 0}, "redk": {"splitk_inkernel": 0}, "no320redk": {"tile_256x320": 0, "splitk_inkernel": 0},
             "halo1": {"halo_pipe": 0}, "halo2": {"halo_pipe": 1}, "pp0": {"gemm_pp": 0}, "pp1": {"gemm_pp": 1}}
