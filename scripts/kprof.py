@@ -51,6 +51,12 @@ def main():
         out = torch.empty(M, 4 * C, dtype=dt, device=dev)
         fn = lambda: L.call("irx_op_gemm_geglu", O.S(), O.DT[dt], M, 8 * C, C, O.P(A), O.P(Wt), O.P(bias),  # noqa: E731
                             O.P(out))
+    elif a.op == "ff1_320":
+        A, Bw = rn(65536, 320), rn(2560, 320, scale=1 / math.sqrt(320))
+        fn = lambda: O.gemm(A, Bw)                                            # noqa: E731
+    elif a.op == "ff2_320":
+        A, Bw = rn(65536, 1280), rn(320, 1280, scale=1 / math.sqrt(1280))
+        fn = lambda: O.gemm(A, Bw)                                            # noqa: E731
     elif a.op == "lin320":
         A, Bw = rn(65536, 320), rn(320, 320, scale=1 / math.sqrt(320))
         fn = lambda: O.gemm(A, Bw)                                            # noqa: E731
