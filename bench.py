@@ -215,6 +215,7 @@ def cpu_baseline_and_parity(eng_bf16, sds, device, n_images: int, threads: int) 
             r = PR.img2img_ref(models, Image.fromarray(noisy[i]), ids_p, ids_n, strength, steps, guidance, 42, "pndm")
             t_img.append(time.perf_counter() - t0)
             refs.append(r)
+            log(f"cpu_baseline: image {i + 1}/{n_images} in {t_img[-1]:.1f} s")   # (progress: one line per image)
     per_img = float(np.mean(t_img))
     cpu = {"value": round(1.0 / per_img, 6), "unit": "images/s", "cores": threads, "kind": "port",
            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
