@@ -1265,6 +1265,7 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   IRX_CHECK(!a.gn_ab || halo_bn(a), "GroupNorm-fused operand needs the halo conv path");
   IRX_CHECK(!a.gn_part || gemm_emits_gn_parts(a), "GroupNorm partials need the large-tile epilogue");
   IRX_CHECK(!a.ln_rs || gemm_ln_foldable(a), "folded LayerNorm needs the large-tile epilogue");
+  if (gemm_sk(a, s)) return true;   // K = 320 streaming path (gemm_sk.hip)
   if (const int hbn = halo_bn(a)) {
     GemmArgs b = a;
     b.vec_epilogue = 1;

@@ -4,7 +4,9 @@ target a single kernel (`--kernel-include-regex`) without the rest of the bench 
 
   python scripts/kprof.py --op conv320      halo 3x3 conv, 64x64 level, 320 -> 320
   python scripts/kprof.py --op geglu320     GEGLU feed-forward projection, M 65536, K 320, N 2560
-  python scripts/kprof.py --op lin320       K = 320 projection (proj_out / to_out), M 65536, N 320
+  python scripts/kprof.py --op lin320       K = 320 projection (proj_in / to_q), M 65536, N 320
+  python scripts/kprof.py --op lin320r      ... + residual (to_out / proj_out)
+  python scripts/kprof.py --op qkv320       q|k|v projection, N 960 (row-major here)
   python scripts/kprof.py --op lin1280      16x16-level projection, M 4096, N 1280, K 1280
   python scripts/kprof.py --op attn40       self-attention, 8 heads x d 40, L 4096
 options: --iters N (default 20), --opt name=value (irx_set_option, repeatable)
@@ -59,6 +61,13 @@ def main():
         fn = lambda: O.gemm(A, Bw)                                            # noqa: E731
     elif a.op == "lin320":
         A, Bw = rn(65536, 320), rn(320, 320, scale=1 / math.sqrt(320))
+        fn = lambda: O.gemm(A, Bw)                                            # noqa: E731
+    elif a.op == "lin320r":                                                    # to_out / proj_out: + residual
+        A, Bw, R = rn(65536, 320), rn(320, 320, scale=1 / math.sqrt(320)), rn(65536, 320)
+        bias = torch.zeros(320, device=dev)
+        fn = lambda: O.gemm(A, Bw, bias=bias, residual=R)                      # noqa: E731
+    elif a.op == "qkv320":
+        A, Bw = rn(65536, 320), rn(960, 320, scale=1 / math.sqrt(320))
         fn = lambda: O.gemm(A, Bw)                                            # noqa: E731
     elif a.op == "lin1280":
         A, Bw = rn(4096, 1280), rn(1280, 1280, scale=1 / math.sqrt(1280))
