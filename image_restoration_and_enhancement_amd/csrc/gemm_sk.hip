@@ -20,12 +20,26 @@
 // the large-tile kernel (alpha / bias or the LayerNorm fold, rounding to the storage type, then residual and
 // out_scale, rounding again; GEGLU h * gelu(g) on the rounded halves) — independent of M, the batch and the
 // tile placement, so the engines stay batch invariant.
+#include <algorithm>
+
 #include "ops.h"
 #include "profile.h"
 
+// timing diagnostics only (a separately built library, scripts/build_skdbg.sh): 1 no epilogue / stores, 2 no MFMAs,
+// 4 no A DMA — results are wrong when set
+#ifndef IRX_SK_DBG
+#define IRX_SK_DBG 0
+#endif
+
 namespace irx {
 
-int g_gemm_sk = 1;   // irx_set_option("gemm_sk", 0): the K = 320 projections take the large-tile kernel (A/B)
+// irx_set_option("gemm_sk", m): 1 (default) the GEGLU projection only, 3 every K = 320 shape, 2 GEGLU on the one-wave-
+// per-SIMD form, 0 none.  Measured (profiles/r03_kprof_sk_n.txt, M = 65536): GEGLU 179 vs 214 us on the large-tile
+// kernel; the N = 320 / 960 projections 32 / 37 / 74 vs 27 / 34 / 66 us — one wave per SIMD with the B slice in
+// registers leaves the MFMA pipe 14 % busy behind AGPR -> VGPR operand copies and the epilogue's VALU work
+// (profiles/r03_pmc_sk_*.txt), so those stay on the large-tile kernel
+int g_gemm_sk = 1;
+int g_gemm_sk_blocks = 0;   // irx_set_option("gemm_sk_blocks", n): persistent blocks per XCD (0: 32 x blocks per CU)
 
 namespace {
 
@@ -73,21 +87,40 @@ constexpr int kSkRC = kSkK / 8;    // 16-byte chunks per A row
 
 // NB: 16-row B blocks per wave (4 waves): 5 -> 320-column slices; GEGLU: 4 (2 value + 2 gate blocks) -> 256 weight
 // rows = 128 output channels per slice.  MB: 16-row blocks per tile (BM = 16 MB rows); BPC: resident blocks per CU
-// (2: two waves per SIMD, the registers of one wave <= 256).  groups: row groups per XCD (blocks of one group share
-// row tiles).
+// (2: two waves per SIMD, the registers of one wave <= 256); RES: residual add (a double-buffered LDS copy of the
+// tile's residual rows, DMA'd one tile ahead); S: A ring stages; AF2: A fragments of the next K step requested before
+// the current step's MFMAs.  groups: row groups per XCD (blocks of one group share row tiles).
+//
+// Every global -> LDS transfer is LDS-DMA issued from inline asm and every wait on it an explicit, exactly counted
+// vmcnt (the loop issues no compiler-visible load, so the compiler adds no wait of its own that would also drain the
+// DMA in flight).  Rows past M in the last tile are bound to tile row (r & 1): they re-read that row's A, residual and
+// LayerNorm statistics, and their store rewrites that row with identical bytes — every DMA and store is issued by
+// every wave, so the counts hold for ragged M too (M even; the host checks it when the statistics are read).
 template <typename T, int NB, bool GEGLU, int MB, int BPC, bool RES, int S, bool AF2>
 __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_slices, int groups) {
   constexpr int BM = 16 * MB, KS = kSkKS, RC = kSkRC;
   constexpr int STAGE = BM * RC;           // uint4 per ring stage (40 KiB at 64 rows)
   constexpr int PPW = STAGE / 64 / 4;      // LDS-DMA pieces (1 KiB wave-instructions) per wave per stage
   static_assert(PPW * 256 == STAGE, "whole pieces per wave");
-  constexpr int NS = 4 * NB * 16;   // weight rows per block
+  constexpr int NS = 4 * NB * 16;          // weight rows per block
   static_assert(!GEGLU || NB == 4, "GEGLU: 2 value + 2 gate blocks per wave");
+  static_assert(!(RES && GEGLU), "no residual on the GEGLU projection");
+  constexpr int OC = GEGLU ? 32 : NB * 16; // output columns per wave
+  constexpr int CH = OC / 8;               // 16-byte chunks per output row piece
+  constexpr int SRU = CH + 1;              // staging row stride (uint4): 44 / 20 dwords, conflict-free 8-byte writes
+  constexpr int NR = MB / 2;               // 32-row epilogue rounds per tile
+  constexpr int NCK = 32 * CH / 64;        // 16-byte chunks per lane per round
+  static_assert(MB % 2 == 0 && (32 * CH) % 64 == 0, "32-row rounds, whole chunks per lane");
+  constexpr int RESN = RES ? NR * NCK : 0; // residual DMA pieces per wave per tile
+  constexpr int LNL = BM / 8;              // lanes per wave carrying the tile's LayerNorm statistics (16 B = 2 rows)
+  constexpr int SN = NR * NCK;             // epilogue stores per wave per tile
   __shared__ __attribute__((aligned(16))) uint4 ring[S * STAGE];
+  __shared__ __attribute__((aligned(16))) float2 lnring[S * BM];
+  __shared__ __attribute__((aligned(16))) uint4 resbuf[RES ? 2 * 4 * BM * CH : 1];
   __shared__ __attribute__((aligned(16))) float sbias[NS];
   __shared__ __attribute__((aligned(16))) float su[NS];
-  __shared__ __attribute__((aligned(16))) uint4 stage_buf[4 * 32 * ((GEGLU ? 32 : NB * 16) / 8 + 1)];
-  __shared__ long noff_tab[4 * ((GEGLU ? 32 : NB * 16) / 8)];
+  __shared__ __attribute__((aligned(16))) uint4 stage_buf[4 * 32 * SRU];
+  __shared__ long noff_tab[4 * CH];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -99,6 +132,8 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
   const int t0 = lo + grp;
   if (t0 >= hi) return;
   const int nt = (hi - t0 + groups - 1) / groups;   // tiles of this block: t0, t0 + groups, ...
+  const bool has_ln = !RES && a.ln_rs != nullptr;
+  const int PA = PPW + (has_ln ? 1 : 0);            // A-tile DMA pieces per wave (+ the statistics piece)
 
   // weight row (index into B / bias / ln_u) of slice-local row idx
   auto wrow = [&](int idx) -> int {
@@ -115,6 +150,17 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
     sbias[i] = a.bias ? a.bias[n] : 0.f;
     su[i] = a.ln_u ? a.ln_u[n] : 0.f;
   }
+  const int n0w = GEGLU ? sl * 128 + w * 32 : sl * NS + w * OC;   // first output column of this wave
+  long* const ncol = noff_tab + w * CH;   // output-column part of a chunk's address (head-split q|k|v: part/head/e)
+  if (lane < CH) {
+    const int n = n0w + lane * 8;
+    long o = n;
+    if (a.hs_L) {
+      const int part = n / a.hs_C, rm = n - part * a.hs_C, hd = rm / a.hs_d, e = rm - hd * a.hs_d;
+      o = (long)part * a.M * a.hs_C + (long)hd * a.hs_L * a.hs_d + e;
+    }
+    ncol[lane] = o;
+  }
 
   // ---- B slice in registers: bfr[j][kk] = rows (w*NB + j)*16 + (lane & 15), k chunk kk*4 + (lane >> 4)
   uint4 bfr[NB][KS];
@@ -125,14 +171,17 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) bfr[j][kk] = *(const uint4*)(p + kk * 32);
   }
+  // a wait the compiler sees (it then knows bfr has landed and puts no wait for it inside the loop)
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
 
-  // ---- LDS-DMA assignment: piece j of wave w covers ring chunks p = (w*PPW + j)*64 + lane: tile row p / RC,
-  //      physical chunk p % RC, which holds logical chunk (p % RC) ^ (row & 7) (conflict-free b128 fragment reads);
-  //      rows past M re-read row 0 of the tile (their products are never stored)
+  auto tile_of = [&](int it) { return t0 + min(it, nt - 1) * groups; };   // (clamped: surplus issues re-read)
+  auto lds32 = [](const void* p) { return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)p); };
+  // ---- A tile #it -> ring stage it % S: piece j of wave w covers ring chunks p = (w*PPW + j)*64 + lane (tile row
+  //      p / RC, physical chunk p % RC holding logical chunk (p % RC) ^ (row & 7): conflict-free b128 fragment reads);
+  //      with the LayerNorm fold, one more piece: LNL lanes x 16 B of the row statistics
   const uint16_t* Ag = (const uint16_t*)a.A;
-  auto issue = [&](int it) {   // tile #it of this block (clamped: surplus issues re-read the last tile) -> stage
-    const int tt = t0 + min(it, nt - 1) * groups;
-    const long m0 = (long)tt * BM;
+  auto issueA = [&](int it) {
+    const long m0 = (long)tile_of(it) * BM;
     const int rem = a.M - (int)m0;
     const uint16_t* base = Ag + m0 * a.lda;
     uint4* st = ring + (it % S) * STAGE + w * PPW * 64;
@@ -140,91 +189,71 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
     for (int j = 0; j < PPW; ++j) {
       const int p = (w * PPW + j) * 64 + lane;
       const int r = p / RC, c = (p % RC) ^ (r & 7);
-      const uint16_t* src = base + (r < rem ? r * a.lda : 0) + c * 8;
-      glds16(src, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)(st + j * 64)));
+      glds16(base + (r < rem ? r : (r & 1)) * a.lda + c * 8, lds32(st + j * 64));
     }
-  };
-
-  // ---- epilogue layout.  Phase 1 (per 32-row round): each lane turns its accumulators (4 consecutive channels of
-  //      one pixel per 16x16 block) into storage-type values — alpha / bias or the LayerNorm fold, rounded; GEGLU
-  //      h * gelu(g) — and writes them as 8-byte pieces into the wave's private staging rows.  Phase 2: the wave reads
-  //      the rows back as 16-byte chunks (lane -> consecutive chunks of consecutive rows), adds the residual chunk
-  //      (prefetched a tile ahead with the same 16-byte pattern), applies out_scale and stores whole 16-byte row
-  //      pieces (the large-tile kernel's two-pass arithmetic).  Staging rows: OC columns + one 16-byte pad (row strides
-  //      of 44 / 20 dwords: conflict-free 8-byte writes).  A wave's rows are its own: no barrier.
-  constexpr int OC = GEGLU ? 32 : NB * 16;   // output columns per wave
-  constexpr int CH = OC / 8;                 // 16-byte chunks per output row piece
-  constexpr int SRU = CH + 1;                // staging row stride (uint4)
-  constexpr int NR = MB / 2;                 // 32-row rounds per tile
-  constexpr int NCK = 32 * CH / 64;          // 16-byte chunks per lane per round
-  static_assert(MB % 2 == 0 && (32 * CH) % 64 == 0, "32-row rounds, whole chunks per lane");
-  uint4* const stg = stage_buf + w * 32 * SRU;
-  const int q4 = (lane >> 4) * 4;
-  const int n0w = GEGLU ? sl * 128 + w * 32 : sl * NS + w * OC;   // first output column of this wave
-  // chunk k of a lane in a round: staging row (lane + 64k) / CH, chunk (lane + 64k) % CH; the output-column part of
-  // its address comes from a per-wave table (head-split q|k|v: part / head / element of the column)
-  auto crow = [&](int k) { return (lane + 64 * k) / CH; };
-  auto cch = [&](int k) { return (lane + 64 * k) % CH; };
-  long* const ncol = noff_tab + w * CH;
-  if (lane < CH) {
-    const int n = n0w + lane * 8;
-    long o = n;
-    if (a.hs_L) {
-      const int part = n / a.hs_C, rm = n - part * a.hs_C, hd = rm / a.hs_d, e = rm - hd * a.hs_d;
-      o = (long)part * a.M * a.hs_C + (long)hd * a.hs_L * a.hs_d + e;
-    }
-    ncol[lane] = o;
-  }
-  static_assert(!(RES && GEGLU), "no residual on the GEGLU projection");
-  constexpr bool has_res = RES;
-  const bool has_ln = !RES && a.ln_rs != nullptr;
-  // loads that run one tile ahead of their use: the residual chunks and the LayerNorm row statistics
-  uint4 rres[RES ? NR : 1][NCK];
-  float2 lrs[RES ? 1 : MB];
-  auto prefetch = [&](int it) {
-    const int tt = t0 + min(it, nt - 1) * groups;
-    const long tm = (long)tt * BM;
     if (has_ln) {
-#pragma unroll
-      for (int i = 0; i < MB; ++i) lrs[i] = a.ln_rs[min(tm + i * 16 + (lane & 15), (long)a.M - 1)];
-    }
-    if constexpr (!GEGLU) {
-      if (has_res) {
-        const uint16_t* R = (const uint16_t*)a.residual + n0w;
-#pragma unroll
-        for (int rr = 0; rr < NR; ++rr)
-#pragma unroll
-          for (int k = 0; k < NCK; ++k)
-            rres[rr][k] = *(const uint4*)(R + min(tm + rr * 32 + crow(k), (long)a.M - 1) * a.ldr + cch(k) * 8);
+      if (lane < LNL) {
+        const int r = 2 * (w * LNL + lane);   // rows r, r + 1 (M even: both valid or both past M)
+        glds16(a.ln_rs + m0 + (r < rem ? r : 0), lds32(lnring + (it % S) * BM + 2 * w * LNL));
       }
     }
   };
-  const int RN = (has_res ? NR * NCK : 0) + (has_ln ? MB : 0);   // prefetch loads per tile (always issued)
+  // ---- residual rows of tile #it -> resbuf[it & 1] (the wave's OC columns; linear chunk p = lane + 64k <-> row p / CH,
+  //      chunk p % CH, the order phase 2 reads them in)
+  auto issueR = [&](int it) {
+    if constexpr (RES) {
+      const long m0 = (long)tile_of(it) * BM;
+      const int rem = a.M - (int)m0;
+      const uint16_t* R = (const uint16_t*)a.residual + m0 * a.ldr + n0w;
+      uint4* dst = resbuf + ((it & 1) * 4 + w) * BM * CH;
+#pragma unroll
+      for (int k = 0; k < RESN; ++k) {
+        const int p = lane + 64 * k, r = p / CH, c = p % CH;
+        glds16(R + (r < rem ? r : (r & 1)) * a.ldr + c * 8, lds32(dst + 64 * k));
+      }
+    }
+  };
+
+  // ---- epilogue.  Phase 1 (per 32-row round): each lane turns its accumulators (4 consecutive channels of one pixel
+  //      per 16x16 block) into storage-type values — alpha / bias or the LayerNorm fold, rounded; GEGLU h * gelu(g) —
+  //      and writes them as 8-byte pieces into the wave's private staging rows.  Phase 2: the wave reads the rows back
+  //      as 16-byte chunks (lane -> consecutive chunks of consecutive rows), adds the residual chunk, applies
+  //      out_scale and stores whole 16-byte row pieces (the large-tile kernel's two-pass arithmetic).  A wave's staging
+  //      rows are its own: no barrier.
+  uint4* const stg = stage_buf + w * 32 * SRU;
+  const int q4 = (lane >> 4) * 4;
+  auto crow = [&](int k) { return (lane + 64 * k) / CH; };
+  auto cch = [&](int k) { return (lane + 64 * k) % CH; };
+  const long rstride = a.hs_L ? a.hs_d : a.ldc;
 
   // fragment read addressing: row (lane & 15) of each 16-row block, logical chunk kk*4 + (lane >> 4), stored at
   // chunk ^ (row & 7) = 8 * (kk >> 1) + 4 * ((kk & 1) ^ hb) + lo
   const int sw = lane & 7, hb = sw >> 2, lo4 = (lane >> 4) ^ (sw & 3);
   const int fb0 = (lane & 15) * RC + 4 * hb + lo4, fb1 = (lane & 15) * RC + 4 * (hb ^ 1) + lo4;
 
+  // issue order: A(0 .. S-2), R(0); per iteration j: R(j + 1), A(j + S - 1), stores(j) — all unconditional
 #pragma unroll
-  for (int p = 0; p < S - 1; ++p) issue(p);
-  prefetch(0);
+  for (int p = 0; p < S - 1; ++p)
+    if constexpr (!(IRX_SK_DBG & 4)) issueA(p);
+  issueR(0);
   for (int it = 0; it < nt; ++it) {
-    // issue order: DMA(0 .. S-2), prefetch(0), then per iteration j: DMA(j + S - 1), stores, prefetch(j + 1).  Younger
-    // than DMA(it) and always issued: (S - 2) DMA tiles and min(it + 1, S - 1) prefetches (the epilogue stores are
-    // never counted: conservative)
-    vm_wait((S - 2) * PPW + min(it + 1, S - 1) * RN);
-    // every wave's pieces of tile it landed; stage (it + S - 1) % S free (lgkmcnt: the bias / u table stores)
+    // A(it) landed: younger are, it <= S-2: (S-2-it) A + R(0) + it (R + A + stores); else stores(it-S+1) + (S-2)
+    // (R + A + stores) (capped at the counter's 63: waiting for a little more is safe)
+    if constexpr (!(IRX_SK_DBG & 4))
+      vm_wait(min(63, it <= S - 2 ? (S - 2 - it) * PA + RESN + it * (RESN + PA + SN)
+                                  : SN + (S - 2) * (RESN + PA + SN)));
+    // every wave's pieces of tile it landed; stage (it + S - 1) % S and resbuf[(it + 1) & 1] free (lgkmcnt: the
+    // bias / column tables before the first use)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    issue(it + S - 1);
+    issueR(it + 1);
+    if constexpr (!(IRX_SK_DBG & 4)) issueA(it + S - 1);
     const uint4* As = ring + (it % S) * STAGE;
     f32x4 acc[NB][MB];
 #pragma unroll
     for (int j = 0; j < NB; ++j)
 #pragma unroll
       for (int i = 0; i < MB; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    {
-      // A fragments of step kk + 1 requested before the MFMAs of step kk (AF2), or per step (register-tight forms)
+    if constexpr (!(IRX_SK_DBG & 2)) {
       constexpr int NAF = AF2 ? 2 : 1;
       uint4 af[NAF][MB];
       auto rdA = [&](int kk, uint4* f) {
@@ -248,14 +277,29 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
         __builtin_amdgcn_s_setprio(0);
       }
     }
+    if constexpr ((IRX_SK_DBG & 1) != 0) {   // diagnostics: keep the accumulators live, skip the epilogue
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int i = 0; i < MB; ++i) t += acc[j][i][0] + acc[j][i][3];
+      if (t == 12345.678f) ((float*)a.C)[lane] = t;
+      continue;
+    }
+
     // ---- epilogue
-    const long tm0 = (long)(t0 + it * groups) * BM;
+    // R(it) landed (the statistics came with A(it)): younger are R(it + 1) + A(it + S - 1), and for it >= 1 also
+    // A(it + S - 2) + stores(it - 1)
+    if constexpr (RES) vm_wait(min(63, it == 0 ? RESN + PA : 2 * PA + SN + RESN));
+    const long tm0 = (long)tile_of(it) * BM;
+    const int rem = a.M - (int)tm0;
     long mbase = tm0 * a.ldc;                  // element offset of the tile's first output row
     if (a.hs_L) {                              // (hs_L % BM == 0: a tile lies in one image)
       const long img = tm0 / a.hs_L;
       mbase = img * a.hs_C * a.hs_L + (tm0 - img * a.hs_L) * a.hs_d;
     }
-    const long rstride = a.hs_L ? a.hs_d : a.ldc;
+    const float2* lst = lnring + (it % S) * BM;
+    const uint4* rsb = resbuf + ((it & 1) * 4 + w) * BM * CH;
     T* Cp = (T*)a.C;
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
@@ -263,7 +307,7 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
 #pragma unroll
       for (int ih = 0; ih < 2; ++ih) {
         const int i = 2 * rr + ih;
-        const float2 rs = has_ln ? lrs[i] : make_float2(1.f, 0.f);
+        const float2 rs = has_ln ? lst[i * 16 + (lane & 15)] : make_float2(1.f, 0.f);
         float v[NB][4];
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
@@ -299,11 +343,12 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
       for (int k = 0; k < NCK; ++k) {
         uint4 u = stg[crow(k) * SRU + cch(k)];
         if constexpr (!GEGLU) {
-          if (has_res || a.out_scale != 1.f) {
-            float f[8], rv[8];
+          if (RES || a.out_scale != 1.f) {
+            float f[8];
             Vec16<T>::unpack(u, f);
-            if (has_res) {
-              Vec16<T>::unpack(rres[rr][k], rv);
+            if constexpr (RES) {
+              float rv[8];
+              Vec16<T>::unpack(rsb[rr * 32 * CH + lane + 64 * k], rv);
 #pragma unroll
               for (int e = 0; e < 8; ++e) f[e] += rv[e];
             }
@@ -313,10 +358,10 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
           }
         }
         const int row = rr * 32 + crow(k);
-        if (tm0 + row < a.M) *(uint4*)(Cp + mbase + row * rstride + ncol[cch(k)]) = u;
+        const int srow2 = row < rem ? row : (row & 1);   // rows past M rewrite row (r & 1) with its own bytes
+        *(uint4*)(Cp + mbase + srow2 * rstride + ncol[cch(k)]) = u;
       }
     }
-    if (RN) prefetch(it + 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // surplus DMA pieces land before the block's LDS is released
 }
@@ -325,7 +370,8 @@ template <typename T, int NB, bool GEGLU, int MB, int BPC, bool RES, int S, bool
 void launch_sk(const GemmArgs& a, hipStream_t s) {
   constexpr int NS = 4 * NB * 16;
   const int n_slices = GEGLU ? (a.N / 2) / 128 : a.N / NS;
-  const int groups = 32 * BPC / n_slices;
+  const int per_xcd = std::max(n_slices, g_gemm_sk_blocks > 0 ? g_gemm_sk_blocks : 32 * BPC);
+  const int groups = per_xcd / n_slices;
   const char* tn = std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short";
   std::string nm;
   if (prof_on())
@@ -333,7 +379,7 @@ void launch_sk(const GemmArgs& a, hipStream_t s) {
          (GEGLU ? "true" : "false") + ", " + std::to_string(MB) + ", " + std::to_string(BPC) + ", " +
          (RES ? "true" : "false") + ", " + std::to_string(S) + ", " + (AF2 ? "true" : "false") + ">";
   ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K, s);
-  gemm_sk_kernel<T, NB, GEGLU, MB, BPC, RES, S, AF2><<<256 * BPC, 256, 0, s>>>(a, n_slices, groups);
+  gemm_sk_kernel<T, NB, GEGLU, MB, BPC, RES, S, AF2><<<8 * per_xcd, 256, 0, s>>>(a, n_slices, groups);
   IRX_LAUNCH_CHECK();
 }
 
@@ -343,7 +389,7 @@ void launch_sk(const GemmArgs& a, hipStream_t s) {
 // partials; N a multiple of the 320-column slice (GEGLU: of 256 interleaved weight rows); 16-byte aligned rows.
 // The decision depends only on the per-call shape (not on M), so it is the same for every batch size.
 bool gemm_sk_eligible(const GemmArgs& a) {
-  if (!g_gemm_sk || !is16(a.dtype) || a.conv || a.out_f32 || a.batch != 1 || a.K != kSkK) return false;
+  if (!g_gemm_sk || (!a.geglu && g_gemm_sk != 3) || !is16(a.dtype) || a.conv || a.out_f32 || a.batch != 1 || a.K != kSkK) return false;
   if (a.act != ACT_NONE || a.rowadd || a.gn_part || a.gn_ab) return false;
   if (a.geglu ? (a.N % 256 != 0 || a.N / 2 / 128 > 32 || a.residual || a.hs_L || a.ldc % 4) : (a.N % 320 || a.N / 320 > 32))
     return false;
@@ -351,7 +397,7 @@ bool gemm_sk_eligible(const GemmArgs& a) {
   if (((uintptr_t)a.C % 8) || (a.hs_L ? (a.hs_d % 4 || a.hs_C % 4) : a.ldc % 4)) return false;
   if (a.residual && (a.ldr % 4 || ((uintptr_t)a.residual % 8))) return false;
   if (a.hs_L && (a.residual || a.hs_L % 64)) return false;   // (a 64-row tile lies in one image)
-  if (a.ln_rs && a.alpha != 1.f) return false;
+  if (a.ln_rs && (a.alpha != 1.f || a.M % 2)) return false;   // (statistics DMA'd as row pairs)
   return a.M > 0;
 }
 
@@ -367,9 +413,9 @@ bool gemm_sk(const GemmArgs& a0, hipStream_t s) {
       if (f16) launch_sk<f16_t, 4, true, 2, 2, false, 3, false>(a, s);
       else launch_sk<bf16_t, 4, true, 2, 2, false, 3, false>(a, s);
     }
-  } else if (a.residual) {  // 32-row tiles (the residual chunks of a tile held in registers), a 6-deep ring
-    if (f16) launch_sk<f16_t, 5, false, 2, 1, true, 6, true>(a, s);
-    else launch_sk<bf16_t, 5, false, 2, 1, true, 6, true>(a, s);
+  } else if (a.residual) {  // 32-row tiles, a 4-deep A ring beside the double-buffered residual rows
+    if (f16) launch_sk<f16_t, 5, false, 2, 1, true, 4, true>(a, s);
+    else launch_sk<bf16_t, 5, false, 2, 1, true, 4, true>(a, s);
   } else {
     if (f16) launch_sk<f16_t, 5, false, 4, 1, false, 3, true>(a, s);
     else launch_sk<bf16_t, 5, false, 4, 1, false, 3, true>(a, s);

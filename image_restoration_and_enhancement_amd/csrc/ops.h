@@ -78,6 +78,7 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path
 bool gemm_sk(const GemmArgs& a, hipStream_t s);           // K = 320 streaming path (gemm_sk.hip); false if not eligible
 bool gemm_sk_eligible(const GemmArgs& a);
 extern int g_gemm_sk;      // 1: the K = 320 projections take gemm_sk (0: the large-tile kernel, A/B)
+extern int g_gemm_sk_blocks;
 size_t gemm_workspace_bytes(const GemmArgs& a);           // split-K partial buffer the call will use
 bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can apply the GEGLU epilogue
 bool gemm_gn_fusable(const GemmArgs& a);                  // conv can apply GemmArgs::gn_ab to its operand

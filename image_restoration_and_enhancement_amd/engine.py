@@ -9,6 +9,7 @@ This replaces the reference's `pipe_class.from_pretrained(...).to("cuda")`
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -113,6 +114,9 @@ def _pad_to(t: torch.Tensor, shape: Tuple[int, ...]) -> torch.Tensor:
     for a, b in zip(reversed(t.shape), reversed(shape)):
         pads += [0, b - a]
     return F.pad(t, pads)
+
+
+_POISON = os.environ.get("IRX_WS_POISON", "0") == "1"
 
 
 class NativeModel:
@@ -249,6 +253,8 @@ class UNet(NativeModel):
         if out is None:
             out = torch.empty((B, h, w, self.cfg.out_channels), dtype=torch.float32, device=self.device)
         ws = self.workspace(self.workspace_bytes(B, h, w))
+        if _POISON:   # diagnostics (IRX_WS_POISON=1): every workspace byte 0xFF (a NaN in fp16 / bf16 / fp32) first
+            ws.fill_(255)
         L.call("irx_unet_forward", self.h, self.stream(), C.c_void_p(x.data_ptr()), B, h, w,
                C.c_void_p(t.data_ptr()), C.c_void_p(kv.data_ptr()), ctx_len, C.c_void_p(out.data_ptr()),
                C.c_void_p(ws.data_ptr()), ws.numel())

@@ -46,7 +46,7 @@ def main():
     cmp("vae.encode", lambda u: eng.vae.encode(eng.to_tensor(u.contiguous())), imgs, 3)
     z = (torch.randn(B, h, h, 8, generator=g) * 0.8).to(eng.tdt).to(dev)
     cmp("vae.decode", lambda t: eng.vae.decode(t.contiguous()), z, 3)
-    emb = eng.text_embeddings("clean high quality photo", True)
+    emb = eng.text_embeddings("clean high quality photo, no noise, sharp details", True)
     x = (torch.randn(2 * B, h, h, eng.unet.cin_pad, generator=g)).to(eng.tdt).to(dev)
     t = torch.full((2 * B,), 500.0, device=dev)
 

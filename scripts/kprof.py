@@ -31,8 +31,9 @@ def main():
     ap.add_argument("--op", required=True)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--opt", action="append", default=[])
+    ap.add_argument("--lib", default=None, help="alternate libirx.so (timing-diagnostic builds)")
     a = ap.parse_args()
-    L.load()
+    L.load(a.lib)
     for o in a.opt:
         k, v = o.split("=")
         L.call("irx_set_option", k.encode(), int(v))

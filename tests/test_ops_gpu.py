@@ -617,6 +617,7 @@ def test_attention_v3_vs_v2_and_head_major(device, dt, B, Lq, Lk, C, heads):
 
 
 def _with_sk(v, fn):
+    # v = 3: every K = 320 shape on gemm_sk (the default takes only the GEGLU projection there)
     from image_restoration_and_enhancement_amd import _lib as L
     L.call("irx_set_option", b"gemm_sk", v)
     try:
@@ -640,7 +641,7 @@ def test_gemm_sk(device, M, N, res, dt):
     R = _r(M, N, seed=93) if res else None
     a_d, b_d, r_d = _dev(A, dt, device), _dev(Bw, dt, device), (_dev(R, dt, device) if res else None)
     run = lambda: O.gemm(a_d, b_d, bias=bias.to(device), residual=r_d)       # noqa: E731
-    sk, lt = _with_sk(1, run), _with_sk(0, run)
+    sk, lt = _with_sk(3, run), _with_sk(0, run)
     ref = _q(A, dt) @ _q(Bw, dt).T + bias + (_q(R, dt) if res else 0)
     assert O.rel_err(sk, ref) < TOL[dt]
     _same_as_large_tile(sk, lt, dt)
