@@ -71,6 +71,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gemm_pp") g_gemm_pp = value;
   else if (n == "ln_fold") g_ln_fold = value;
   else if (n == "gemm_sk") g_gemm_sk = value;
+  else if (n == "large_mask") g_large_mask = value;
   else if (n == "gemm_sk_blocks") g_gemm_sk_blocks = value;
   else if (n == "vae_attn_rows") g_vae_attn_rows = value;
   else if (n == "vae_flash") g_vae_flash = value;

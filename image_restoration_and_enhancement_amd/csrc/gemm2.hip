@@ -826,13 +826,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         *(uint4*)(Cp + c_off(a, m, n)) = u;
         return u;
       };
-      if (a.gn_part) {
+      if (a.gn_part && NT >= BN) {
         // GroupNorm partials of the stored output, one per tile row block of BM rows (host: gemm_emits_gn_parts):
         // thread = fixed 8-channel chunk column x a row stride, shifted fp32 sums of the rounded values -> raw
         // fp64 (sum, sum of squares), folded over the row groups through LDS in a fixed order.
         constexpr int RS = NT / CPR;                 // row groups
-        constexpr int TPC = NT / BN;                 // fold threads per column (first round)
-        static_assert(TPC >= 1 && RS * BN * 16 <= SMEM * 16, "GroupNorm partial staging");
+        constexpr int TPC = NT >= BN ? NT / BN : 1;  // fold threads per column (first round)
+        static_assert(NT < BN || (TPC >= 1 && RS * BN * 16 <= SMEM * 16), "GroupNorm partial staging");
         const int cc = tid % CPR, rg = tid / CPR;
         const bool colok = rg < RS && n0 + cc * 8 < a.N;
         double2* red = (double2*)smem;
@@ -1061,7 +1061,8 @@ Choice choose(const GemmArgs& a) {
   }
   if (g_gemm_force > 0 && g_gemm_deep == 0) {   // tuning sweeps: BM*100000 + BN*100 + splits
     const int BM = g_gemm_force / 100000, BN = (g_gemm_force / 100) % 1000, sp = g_gemm_force % 100;
-    const bool ok = (BM == 256 || BM == 128) && (BN == 320 || BN == 256 || BN == 128) && a.N % BN == 0 &&
+    const bool ok = (BM == 256 || BM == 128 || (BM == 64 && BN == 320 && sp == 1 && !a.gn_part)) &&
+                    (BN == 320 || BN == 256 || BN == 128) && a.N % BN == 0 &&
                     sp >= 1 && (sp == 1 || !((a.out_f32 && canon_batch(a) > 1) || a.geglu)) && (!a.geglu || BN % 128 == 0) &&
                     !(BM == 256 && BN == 128);   // (256x128 is a 4x2-wave shape: not forced)
     if (ok) {
@@ -1142,6 +1143,7 @@ bool vec_ok(const GemmArgs& a) {
 
 bool eligible(const GemmArgs& a) {
   const int bk = step_k();
+  if (!(g_large_mask & (a.conv ? 2 : 1))) return false;   // (A/B: large tiles for dense GEMMs / convs only)
   if (a.hs_L && !vec_ok(a)) return false;  // head-split stores: the 16-byte LDS-staged epilogue only
   if (a.act != ACT_NONE) return false;   // activations are fused by the 4-wave kernel only (tiny GEMMs)
   // the unrolled scalar (non-16-byte) epilogue only scales and adds bias: row add / residual need vec rows
@@ -1157,6 +1159,7 @@ bool eligible(const GemmArgs& a) {
 
 }  // namespace
 
+int g_large_mask = 3;  // irx_set_option("large_mask", m): bit 0 dense GEMMs, bit 1 convs take the large tiles
 int g_gemm_deep = 0;   // irx_set_option("gemm_deep", m): 0 two-stage BK 64, 1 BK-32 ring, 2 BK-64 3/4-stage ring
 int g_gemm_dbg = 0;
 bool g_gemm_small = false;   // irx_set_option("gemm_small", 1): 4-wave 128x160 / 128x128 tiles for K <= kmax
@@ -1310,6 +1313,11 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     if (sp.inkernel) sp.cnt = stream_counters(s);
   } else {
     sp.per = a.K / step_k();
+  }
+  if (c.BM == 64) {   // 64x320, 4 waves, BK 32, two stages (48 KiB of LDS: three blocks per CU)
+    sp.per = a.K / 32;
+    launch2<64, 320, 1, 4, 32, 2>(b, sp, s);
+    return true;
   }
   if (c.small) {
     if (c.BN == 160) launch2<128, 160, 2, 2, 64, 2>(b, sp, s);
