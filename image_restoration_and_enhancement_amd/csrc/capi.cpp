@@ -50,6 +50,10 @@ static const X* as(const irx_model* h, int kind) {
   return static_cast<const X*>(h->m.get());
 }
 
+// images spanned by the rows of irx_op_gemm / irx_op_gemm_geglu (0: not image-indexed; tests of the canonical-batch
+// tile policy set it through irx_set_option("op_imgs", n))
+static int g_op_imgs = 0;
+
 extern "C" {
 
 const char* irx_last_error(void) { return last_error(); }
@@ -72,6 +76,9 @@ int irx_set_option(const char* name, int value) {
   else if (n == "ln_fold") g_ln_fold = value;
   else if (n == "gemm_sk") g_gemm_sk = value;
   else if (n == "large_mask") g_large_mask = value;
+  else if (n == "large_dense") g_large_dense = value;
+  else if (n == "arena_guard") g_arena_guard = value;
+  else if (n == "op_imgs") g_op_imgs = value;
   else if (n == "gemm_sk_blocks") g_gemm_sk_blocks = value;
   else if (n == "vae_attn_rows") g_vae_attn_rows = value;
   else if (n == "vae_flash") g_vae_flash = value;
@@ -526,6 +533,7 @@ int irx_op_gemm(void* s, int dtype, int M, int N, int K, const void* A, long lda
   a.residual = residual; a.ldr = ldr; a.sR = sR;
   a.out_f32 = out_f32;
   a.batch = batch > 0 ? batch : 1;
+  a.imgs = g_op_imgs;
   gemm(a, S(s));
   IRX_API_END
 }
@@ -621,6 +629,7 @@ int irx_op_gemm_geglu(void* s, int dtype, int M, int N, int K, const void* A, co
   a.dtype = dtype; a.M = M; a.N = N; a.K = K;
   a.A = A; a.lda = K; a.B = B; a.ldb = K;
   a.C = C; a.ldc = N / 2; a.bias = bias; a.geglu = 1;
+  a.imgs = g_op_imgs;
   IRX_CHECK(gemm_geglu_fusable(a), "shape/dtype not eligible for the fused GEGLU epilogue");
   gemm(a, S(s));
   IRX_API_END

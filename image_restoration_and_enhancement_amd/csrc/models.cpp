@@ -15,14 +15,19 @@
 #include "models.h"
 
 #include <cmath>
+#include <cstdio>
+#include <vector>
 
 namespace irx {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ---------------------------------------------------------------------------------------------- Arena
+int g_arena_guard = 0;
+constexpr size_t kGuard = 64 * 1024;
+
 void* Arena::alloc(size_t bytes) {
-  bytes = align_up(bytes ? bytes : 1, 256);
+  bytes = align_up(bytes ? bytes : 1, 256) + (g_arena_guard ? kGuard : 0);
   size_t off = (size_t)-1;
   for (auto it = free_.begin(); it != free_.end(); ++it) {
     if (it->second >= bytes) {
@@ -40,6 +45,12 @@ void* Arena::alloc(size_t bytes) {
   }
   if (base_ && end_ > cap_) throw Error("workspace too small: need > " + std::to_string(end_) + " bytes");
   live_[off] = bytes;
+  ids_[off] = next_id_++;
+  if (g_arena_guard && base_) {
+    IRX_HIP(hipDeviceSynchronize());
+    IRX_HIP(hipMemset(base_ + off + bytes - kGuard, 0xA5, kGuard));
+    IRX_HIP(hipDeviceSynchronize());
+  }
   return base_ ? (void*)(base_ + off) : (void*)(uintptr_t)(off + 4096);
 }
 
@@ -49,6 +60,16 @@ void Arena::free(void* p) {
   auto it = live_.find(off);
   if (it == live_.end()) throw Error("workspace: double free");
   size_t o = off, sz = it->second;
+  if (g_arena_guard && base_) {
+    std::vector<unsigned char> h(kGuard);
+    IRX_HIP(hipDeviceSynchronize());
+    IRX_HIP(hipMemcpy(h.data(), base_ + off + sz - kGuard, kGuard, hipMemcpyDeviceToHost));
+    size_t bad = 0, first = kGuard;
+    for (size_t i = 0; i < kGuard; ++i)
+      if (h[i] != 0xA5) { ++bad; if (first == kGuard) first = i; }
+    if (bad) fprintf(stderr, "arena guard: allocation #%d (%zu bytes) overrun: %zu guard bytes changed, first at +%zu\n",
+                     ids_[off], sz - kGuard, bad, first);
+  }
   live_.erase(it);
   auto nx = free_.lower_bound(o);
   if (nx != free_.end() && nx->first == o + sz) { sz += nx->second; free_.erase(nx); }

@@ -17,7 +17,7 @@ extern int g_vae_flash;       // VAE mid-block attention in the 16-bit engines: 
 class Arena {
  public:
   void reset(char* base, size_t cap) {
-    base_ = base; cap_ = cap; end_ = 0; peak_ = 0; free_.clear(); live_.clear();
+    base_ = base; cap_ = cap; end_ = 0; peak_ = 0; free_.clear(); live_.clear(); ids_.clear(); next_id_ = 0;
   }
   void* alloc(size_t bytes);
   void free(void* p);
@@ -29,7 +29,12 @@ class Arena {
   size_t cap_ = 0, end_ = 0, peak_ = 0;
   std::map<size_t, size_t> free_;    // offset -> size of free holes below end_
   std::map<size_t, size_t> live_;    // offset -> size
+  std::map<size_t, int> ids_;        // offset -> allocation index (guard diagnostics)
+  int next_id_ = 0;
 };
+// diagnostics (irx_set_option("arena_guard", 1)): every workspace allocation is followed by a 64 KiB guard filled with
+// 0xA5, checked when the allocation is freed (device-synchronous; reports overruns on stderr)
+extern int g_arena_guard;
 
 struct P { size_t off = 0; bool set = false; };   // parameter reference into the weight blob
 

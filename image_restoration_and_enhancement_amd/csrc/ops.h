@@ -89,6 +89,7 @@ extern int g_gn_parts;     // 1: producers emit GroupNorm partial sums, the stat
 extern int g_gn_fuse;      // 1: GroupNorm(+SiLU) folded into the following halo conv where it fits (0: A/B)
 extern bool g_large_tiles;
 extern int g_large_mask;
+extern int g_large_dense;
 extern int g_gemm_deep;    // large-tile pipeline: 0 two-stage BK 64, 1 BK-32 S-stage ring, 2 BK-64 deeper ring
 extern int g_gemm_dbg;     // timing diagnostics only: results are wrong when set
 extern bool g_gemm_small;  // short-K GEMMs on 4-wave 128x160 / 128x128 tiles, 2 blocks per CU

@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--dtype", default="fp16")
     ap.add_argument("--res", type=int, default=256)
     ap.add_argument("--opt", action="append", default=[])
+    ap.add_argument("--split", type=int, default=3, help="first part size (of 8)")
     a = ap.parse_args()
     L.load()
     for o in a.opt:
@@ -65,14 +66,15 @@ def main():
     eng.use_graphs = False
     imgs = torch.from_numpy(np.stack([MC.smooth_image(a.res, a.res, seed=50 + i) for i in range(8)])).to(dev)
     W = stages(eng, imgs.contiguous(), 2)
-    P1, P2 = stages(eng, imgs[:3].contiguous(), 2), stages(eng, imgs[3:].contiguous(), 2)
+    c = a.split
+    P1, P2 = stages(eng, imgs[:c].contiguous(), 2), stages(eng, imgs[c:].contiguous(), 2)
     for k in W:
         dim = 1 if k.startswith("eps") or k == "kv" else 0
         p = torch.cat([P1[k], P2[k]], dim=dim)
         d = (W[k].float() - p.float()).abs()
         d = d.flatten(dim + 1).amax(-1)
         nan = int((~torch.isfinite(W[k].float())).sum()) + int((~torch.isfinite(p.float())).sum())
-        print(f"{a.dtype} {a.res} {a.opt} {k}: non-finite {nan}, max|d| {['%.3g' % v for v in d.flatten().tolist()]}",
+        print(f"{a.dtype} {a.res} split {a.split} {a.opt} {k}: non-finite {nan}, max|d| {['%.3g' % v for v in d.flatten().tolist()]}",
               flush=True)
 
 

@@ -38,10 +38,15 @@ def main():
                     L.call("irx_op_gemm_geglu", O.S(), O.DT[dt], a.shape[0], N, K, O.P(a), O.P(Wp), O.P(bp), O.P(out))
                     return out
                 return O.gemm(a, W, bias=bias, residual=r)
+            L.call("irx_set_option", b"op_imgs", 16)
             whole = run(A, R)
             c = 6 * hw
-            parts = torch.cat([run(A[:c].contiguous(), R[:c].contiguous() if R is not None else None),
-                               run(A[c:].contiguous(), R[c:].contiguous() if R is not None else None)])
+            L.call("irx_set_option", b"op_imgs", 6)
+            p1 = run(A[:c].contiguous(), R[:c].contiguous() if R is not None else None)
+            L.call("irx_set_option", b"op_imgs", 10)
+            p2 = run(A[c:].contiguous(), R[c:].contiguous() if R is not None else None)
+            L.call("irx_set_option", b"op_imgs", 0)
+            parts = torch.cat([p1, p2])
             d = (whole.float() - parts.float()).abs().view(16, hw, -1).amax(dim=(1, 2))
             print(f"{dt} {kind} hw {hw} K {K} N {N}: rows differing {int((d > 0).sum())}/16, max {float(d.max()):.3g}",
                   flush=True)
