@@ -111,7 +111,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   const int tiles_n = a.N / BN + (a.N % BN != 0);
   const int tiles_m = (a.M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tile_n = bid % tiles_n, tile_m = bid / tiles_n;
+  const int tile_n = a.nmajor ? bid / tiles_m : bid % tiles_n;
+  const int tile_m = a.nmajor ? bid % tiles_m : bid / tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int z = blockIdx.y / sp.splits, ks = blockIdx.y % sp.splits;
   const int nk_all = a.K / BK;
@@ -1165,6 +1166,7 @@ bool eligible(const GemmArgs& a) {
 
 int g_large_dense = 63;  // irx_set_option("large_dense", m): dense classes on large tiles: 1 N <= 1280, 2 head-split,
                          // GEGLU at K 4: 320, 16: 640, 32: >= 1280, 8 other
+int g_gemm_nmajor = 1;
 int g_large_mask = 3;  // irx_set_option("large_mask", m): bit 0 dense GEMMs, bit 1 convs take the large tiles
 int g_gemm_deep = 0;   // irx_set_option("gemm_deep", m): 0 two-stage BK 64, 1 BK-32 ring, 2 BK-64 3/4-stage ring
 int g_gemm_dbg = 0;
@@ -1310,6 +1312,9 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   GemmArgs b = a;
   b.vec_epilogue = vec_ok(a);
   b.dbg = g_gemm_dbg;
+  // tile order (scheduling only, no numeric effect): N-major when the weights outweigh the activation rows, so that an
+  // XCD's consecutive tiles re-use one B panel from its L2 instead of every XCD streaming all of B
+  b.nmajor = g_gemm_nmajor == 2 || (g_gemm_nmajor == 1 && (long)a.N * a.batch > (long)a.M * a.batch);
   if (a.geglu && !b.vec_epilogue) return false;
   Split sp;
   sp.splits = c.splits;

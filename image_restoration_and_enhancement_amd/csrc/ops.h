@@ -61,6 +61,9 @@ struct GemmArgs {
   // exactly LN(x) W^T + bias, with no normalised copy of A written or read.
   const float2* ln_rs = nullptr; const float* ln_u = nullptr;
   void* splitk_ws = nullptr; size_t splitk_ws_bytes = 0;   // caller workspace for split-K partials
+  // (set by the launcher) N-major tile order: consecutive tiles (one XCD's range) share a B panel instead of an A
+  // panel — for the weight-heavy small-M shapes (8x8-level convs: 29.5 MB of weights for 1024 rows)
+  int nmajor = 0;
   int dbg = 0;            // large-tile diagnostics (irx_set_option("gemm_dbg")): 1 skip epilogue, 2 skip MFMAs
 };
 constexpr int kCanonImages = 16;
@@ -90,6 +93,7 @@ extern int g_gn_fuse;      // 1: GroupNorm(+SiLU) folded into the following halo
 extern bool g_large_tiles;
 extern int g_large_mask;
 extern int g_large_dense;
+extern int g_gemm_nmajor;   // 0 M-major tile order, 1 N-major where B outweighs A (default), 2 always N-major
 extern int g_gemm_deep;    // large-tile pipeline: 0 two-stage BK 64, 1 BK-32 S-stage ring, 2 BK-64 deeper ring
 extern int g_gemm_dbg;     // timing diagnostics only: results are wrong when set
 extern bool g_gemm_small;  // short-K GEMMs on 4-wave 128x160 / 128x128 tiles, 2 blocks per CU

@@ -21,6 +21,7 @@ CONVS = [  # (label, N, H, W, C0, C1, Cout, k, stride, up)
     ("conv640@32", 16, 32, 32, 640, 0, 640, 3, 1, None),
     ("conv1280@16", 16, 16, 16, 1280, 0, 1280, 3, 1, None),
     ("conv1280@8", 16, 8, 8, 1280, 0, 1280, 3, 1, None),
+    ("cat1280+1280->1280@8", 16, 8, 8, 1280, 1280, 1280, 3, 1, None),
     ("cat640+320->320@64", 16, 64, 64, 640, 320, 320, 3, 1, None),
     ("cat320+320->320@64", 16, 64, 64, 320, 320, 320, 3, 1, None),
     ("cat1280+1280->1280@16", 16, 16, 16, 1280, 1280, 1280, 3, 1, None),
@@ -79,7 +80,8 @@ def main():
             "gemm_pp": 0}
     allv = {"s2": {}, "ring64": {"gemm_deep": 2}, "ring32": {"gemm_deep": 1}, "small": {"gemm_small": 1}, "4wave": {"large_tiles": 0},
             "no320": {"tile_256x320": 0}, "redk": {"splitk_inkernel": 0}, "no320redk": {"tile_256x320": 0, "splitk_inkernel": 0},
-            "halo1": {"halo_pipe": 0}, "halo2": {"halo_pipe": 1}, "pp0": {"gemm_pp": 0}, "pp1": {"gemm_pp": 1}}
+            "halo1": {"halo_pipe": 0}, "halo2": {"halo_pipe": 1}, "pp0": {"gemm_pp": 0}, "pp1": {"gemm_pp": 1},
+            "nm0": {"gemm_nmajor": 0}, "nm1": {"gemm_nmajor": 1}, "nm2": {"gemm_nmajor": 2}}
     variants = [(v, allv[v]) for v in args.variants.split(",")]
 
     def setv(opts):
