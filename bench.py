@@ -343,7 +343,7 @@ def main():
         if rank == 0:
             log(f"profiled {args.steps} steps: {tot_fl / 1e12 / (args.steps * batch):.2f} TFLOP/img counted, "
                 f"MFMA-kernel time {tot_ms / args.steps:.1f} ms/step")
-            for name, cnt, ms, fl in prof[:24]:
+            for name, cnt, ms, fl in prof[:int(os.environ.get("IRX_PROF_TOP", "24"))]:
                 log(f"  {ms / args.steps:8.1f} ms/step {cnt // args.steps:5d} launches/step "
                     f"{fl / ms / 1e9 if ms else 0:7.1f} TF/s  {name}")
         name, cnt, ms, fl = next(p for p in prof if p[3] > 0)   # dominant MFMA kernel

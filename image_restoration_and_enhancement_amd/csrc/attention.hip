@@ -947,7 +947,10 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
   dim3 grid(nq * a.H * a.B), block(256);
   ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn3_kernel<") +
                                (std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short") + ", " +
-                               std::to_string(D) + ", " + std::to_string(KT) + ", " + (CAUSAL ? "true" : "false") + ">"
+                               std::to_string(D) + ", " + std::to_string(KT) + ", " + (CAUSAL ? "true" : "false") + ">" +
+                               (g_prof_shapes ? " [B " + std::to_string(a.B) + " Lq " + std::to_string(a.Lq) + " Lk " +
+                                                    std::to_string(a.Lk) + "]"
+                                              : std::string())
                          : std::string(),
                4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
   AttnArgs b = a;

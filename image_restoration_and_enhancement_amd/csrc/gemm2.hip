@@ -1000,6 +1000,10 @@ void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
          std::to_string(BN) + ", " + std::to_string(WM) + ", " + std::to_string(WN) + ", " + std::to_string(BK) + ", " +
          std::to_string(S) + ", " + (a.conv ? "true" : "false") + ", " + (a.out_f32 ? "true" : "false") + ", " +
          (rs ? "true" : "false") + ", " + std::to_string(HALO) + ", " + (PP ? "true" : "false") + ">";
+  if (prof_on() && g_prof_shapes)
+    nm += " [M " + std::to_string(a.M) + " N " + std::to_string(a.N) + " K " + std::to_string(a.K) +
+          (a.conv ? " conv " + std::to_string(a.g.Hin) + "x" + std::to_string(a.g.Win) : std::string()) +
+          " split " + std::to_string(sp.splits) + (a.geglu ? " geglu" : "") + "]";
   {
     ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
     if constexpr (HALO != 0) {

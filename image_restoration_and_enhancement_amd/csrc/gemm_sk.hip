@@ -378,6 +378,8 @@ void launch_sk(const GemmArgs& a, hipStream_t s) {
     nm = std::string("irx::(anonymous namespace)::gemm_sk_kernel<") + tn + ", " + std::to_string(NB) + ", " +
          (GEGLU ? "true" : "false") + ", " + std::to_string(MB) + ", " + std::to_string(BPC) + ", " +
          (RES ? "true" : "false") + ", " + std::to_string(S) + ", " + (AF2 ? "true" : "false") + ">";
+  if (prof_on() && g_prof_shapes)
+    nm += " [M " + std::to_string(a.M) + " N " + std::to_string(a.N) + " K " + std::to_string(a.K) + "]";
   ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K, s);
   gemm_sk_kernel<T, NB, GEGLU, MB, BPC, RES, S, AF2><<<8 * per_xcd, 256, 0, s>>>(a, n_slices, groups);
   IRX_LAUNCH_CHECK();

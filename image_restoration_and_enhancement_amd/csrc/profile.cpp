@@ -10,6 +10,7 @@
 #include "profile.h"
 
 namespace irx {
+int g_prof_shapes = 0;
 namespace {
 struct Rec {
   std::string name;

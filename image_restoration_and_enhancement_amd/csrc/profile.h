@@ -6,6 +6,7 @@
 
 namespace irx {
 bool prof_on();
+extern int g_prof_shapes;   // irx_set_option("prof_shapes", 1): profiler keys carry the call shape (per-shape tables)
 int prof_start(const std::string& name, double flops, hipStream_t s);   // -1 when profiling is off
 void prof_stop(int idx, hipStream_t s);
 void prof_begin();
