@@ -673,6 +673,7 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
     for (int c = 0; c < NSUB; ++c)
 #pragma unroll
       for (int k = 0; k < 16; ++k) sacc[c][k] = init;
+    if (a.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
@@ -680,6 +681,7 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
         const uint4 kf = *(const uint4*)(Ks + (c * 32 + r) * SK + 16 * s + 8 * hh);
         sacc[c] = Mfma<T>::m32x32x16(kf, qf[s], sacc[c]);
       }
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
     if (j0 + KT > a.Lk || (CAUSAL && j0 + KT - 1 > q0)) {
 #pragma unroll
       for (int c = 0; c < NSUB; ++c)
@@ -749,7 +751,9 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
           const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + (krow + 8) * SV + col));
           const uint4 vf = make_uint4(__builtin_bit_cast(uint2, t1).x, __builtin_bit_cast(uint2, t1).y,
                                       __builtin_bit_cast(uint2, t2).x, __builtin_bit_cast(uint2, t2).y);
+          if (a.prio) __builtin_amdgcn_s_setprio(1);
           oacc[dt] = Mfma<T>::m32x32x16(vf, pb[s2], oacc[dt]);
+          if (a.prio) __builtin_amdgcn_s_setprio(0);
         }
     }
     // tile j+1 (registers since last iteration) into the other stage, last read in iteration it-1: every wave
@@ -955,6 +959,7 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
                4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
   AttnArgs b = a;
   b.xcd = g_attn_xcd;
+  b.prio = g_attn_prio;
   attn3_kernel<T, D, KT, CAUSAL><<<grid, block, 0, s>>>(b);
   IRX_LAUNCH_CHECK();
 }
@@ -1048,6 +1053,7 @@ void attention(const AttnArgs& a, hipStream_t s) {
 }
 int g_attn_v3 = 1;
 int g_attn_xcd = 1;
+int g_attn_prio = 0;   // irx_set_option("attn_prio", 1): MFMA chains of attn3 at raised wave priority (A/B)
 int g_attn_hm = 1;
 
 bool g_attn_v2 = true;

@@ -76,6 +76,9 @@ def main():
     elif a.op == "attn40":
         q, k, v = rn(16, 4096, 320), rn(16, 4096, 320), rn(16, 4096, 320)
         fn = lambda: O.attention(q, k, v, 8)                                  # noqa: E731
+    elif a.op == "cross40":
+        q, k, v = rn(16, 4096, 320), rn(16, 77, 320), rn(16, 77, 320)
+        fn = lambda: O.attention(q, k, v, 8)                                  # noqa: E731
     else:
         raise SystemExit(f"unknown op {a.op}")
     for _ in range(3):
