@@ -70,6 +70,9 @@ def main():
     elif a.op == "qkv320":
         A, Bw = rn(65536, 320), rn(960, 320, scale=1 / math.sqrt(320))
         fn = lambda: O.gemm(A, Bw)                                            # noqa: E731
+    elif a.op == "lin640":
+        A, Bw = rn(16384, 640), rn(640, 640, scale=1 / math.sqrt(640))
+        fn = lambda: O.gemm(A, Bw)                                            # noqa: E731
     elif a.op == "lin1280":
         A, Bw = rn(4096, 1280), rn(1280, 1280, scale=1 / math.sqrt(1280))
         fn = lambda: O.gemm(A, Bw)                                            # noqa: E731
