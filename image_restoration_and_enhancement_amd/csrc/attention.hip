@@ -539,7 +539,7 @@ template <int D, int KT> constexpr int attn3_occ() {
   return D <= 40 ? (KT <= 64 ? 4 : 3) : D <= 64 ? (KT <= 64 ? 3 : 2) : D <= 80 ? 2 : 1;
 }
 
-template <typename T, int D, int KT, bool CAUSAL>
+template <typename T, int D, int KT, bool CAUSAL, bool RES>
 __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnArgs a) {
   constexpr int QB = 128;                                  // queries per block (4 waves x 32)
   constexpr int DQ = (D + 15) / 16 * 16, NS = DQ / 16;     // QK^T contraction, 16-deep k-steps
@@ -559,13 +559,15 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5, g = lane >> 4;
-  const int nq = (a.Lq + QB - 1) / QB;
+  // RES (host: non-causal, Lk <= 2 KT — the cross-attention's 77 text tokens): the whole K/V sits in the two LDS
+  // stages, staged once; the block then runs qrep groups of QB queries against it with no barrier in the loop
+  static_assert(!(RES && CAUSAL), "resident K/V is non-causal only");
+  const int qrep = RES && a.qrep > 1 ? a.qrep : 1;
+  const int nq = (a.Lq + QB * qrep - 1) / (QB * qrep);
   const int nblk = nq * a.H * a.B;
   const int lid = a.xcd ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
   const int qb = lid % nq, bh = lid / nq;
   const int b = bh / a.H, h = bh - b * a.H;
-  const int q0 = qb * QB + wave * 32;
-  const int qrow = q0 + r;
   const T* __restrict__ Q = (const T*)a.q + (long)b * a.sq + (long)h * (a.hsq ? a.hsq : D);
   const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : D);
   const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : D);
@@ -574,45 +576,6 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
   for (int i = tid; i < 2 * KT * SK; i += 256) Ks2[i] = (DQ > D && i % SK == D) ? one_bits<T>() : (uint16_t)0;
   for (int i = tid; i < 2 * KT * SV; i += 256) Vs2[i] = (ONES && i % SV == D) ? one_bits<T>() : (uint16_t)0;
 
-  // Q^T fragments (B operand): lane (r, hh) holds q[qrow][16s + 8hh .. +7], pre-scaled by scale*log2(e)
-  uint4 qf[NS];
-  const float sl2 = a.scale * 1.4426950408889634f;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int e = 16 * s + 8 * hh;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (qrow < a.Lq && e < D) v = *(const uint4*)(Q + (long)qrow * a.ldq + e);
-    if (!a.q_scaled) {
-      float f[8];
-      Vec16<T>::unpack(v, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] *= sl2;
-      v = Vec16<T>::pack(f);
-    }
-    qf[s] = v;
-  }
-
-  f32x16 oacc[NDT];
-#pragma unroll
-  for (int i = 0; i < NDT; ++i)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) oacc[i][k] = 0.f;
-  // m: the running max, always a value of the storage type (so -m is exact in a 16-bit operand).
-  // PADM (d < the 16-padded contraction): -m rides in the zero padding as one more k: K[.][d] = 1 (in LDS),
-  // Q[q][d] = -m (lane half 1, k-step NS-1, element 0), so the MFMA chain itself yields S - m.  Otherwise
-  // the accumulators start at -m.
-  constexpr bool PADM = DQ > D;
-  constexpr int PADS = D / 16, PADE = (D % 16) - 8;   // k-step and element of column d in lane half 1
-  static_assert(!PADM || (D % 16 == 8 && PADE == 0), "pad column at element 0 of lane half 1");
-  float m = 0.f, lsum = 0.f;
-  bool first = true;
-  auto set_qpad = [&]() {   // Q^T fragment element holding -m (lane half 1 only; lane half 0 holds d-8 .. d-1)
-    if constexpr (PADM) {
-      if (hh) qf[PADS].x = (qf[PADS].x & 0xFFFF0000u) | (Mfma<T>::pack2(-m, 0.f) & 0xFFFFu);
-    }
-  };
-
-  const int kend = CAUSAL ? min(a.Lk, qb * QB + QB) : a.Lk;
   // per-thread staging slots (row, 16-byte chunk) of a K/V tile, fixed for the kernel: pointers and LDS offsets
   // computed once; a full tile (every row < Lk) loads with no per-row checks
   uint4 kreg[NCH], vreg[NCH];
@@ -656,11 +619,66 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
         *(uint4*)(Vs2 + buf * KT * SV + vsoff[u]) = vreg[u];
       }
   };
-  load(0);
-  __syncthreads();          // pad-column initialisation complete
-  stage(0);
-  __syncthreads();
-  if (KT < kend) load(KT);
+  if constexpr (RES) {
+    load(0);
+    __syncthreads();          // pad-column initialisation complete
+    stage(0);
+    if (KT < a.Lk) {
+      load(KT);
+      stage(1);
+    }
+    __syncthreads();
+  }
+
+  for (int rep = 0; rep < qrep; ++rep) {
+  const int q0 = (qb * qrep + rep) * QB + wave * 32;
+  const int qrow = q0 + r;
+  // Q^T fragments (B operand): lane (r, hh) holds q[qrow][16s + 8hh .. +7], pre-scaled by scale*log2(e)
+  uint4 qf[NS];
+  const float sl2 = a.scale * 1.4426950408889634f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int e = 16 * s + 8 * hh;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (qrow < a.Lq && e < D) v = *(const uint4*)(Q + (long)qrow * a.ldq + e);
+    if (!a.q_scaled) {
+      float f[8];
+      Vec16<T>::unpack(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= sl2;
+      v = Vec16<T>::pack(f);
+    }
+    qf[s] = v;
+  }
+
+  f32x16 oacc[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) oacc[i][k] = 0.f;
+  // m: the running max, always a value of the storage type (so -m is exact in a 16-bit operand).
+  // PADM (d < the 16-padded contraction): -m rides in the zero padding as one more k: K[.][d] = 1 (in LDS),
+  // Q[q][d] = -m (lane half 1, k-step NS-1, element 0), so the MFMA chain itself yields S - m.  Otherwise
+  // the accumulators start at -m.
+  constexpr bool PADM = DQ > D;
+  constexpr int PADS = D / 16, PADE = (D % 16) - 8;   // k-step and element of column d in lane half 1
+  static_assert(!PADM || (D % 16 == 8 && PADE == 0), "pad column at element 0 of lane half 1");
+  float m = 0.f, lsum = 0.f;
+  bool first = true;
+  auto set_qpad = [&]() {   // Q^T fragment element holding -m (lane half 1 only; lane half 0 holds d-8 .. d-1)
+    if constexpr (PADM) {
+      if (hh) qf[PADS].x = (qf[PADS].x & 0xFFFF0000u) | (Mfma<T>::pack2(-m, 0.f) & 0xFFFFu);
+    }
+  };
+
+  const int kend = CAUSAL ? min(a.Lk, qb * QB + QB) : a.Lk;
+  if constexpr (!RES) {
+    load(0);
+    __syncthreads();          // pad-column initialisation complete
+    stage(0);
+    __syncthreads();
+    if (KT < kend) load(KT);
+  }
 
   for (int j0 = 0, it = 0; j0 < kend; j0 += KT, ++it) {
     const uint16_t* Ks = Ks2 + (it & 1) * KT * SK;
@@ -758,9 +776,11 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
     }
     // tile j+1 (registers since last iteration) into the other stage, last read in iteration it-1: every wave
     // has passed the barrier that ended it-1
-    if (j0 + KT < kend) stage((it + 1) & 1);
-    __syncthreads();
-    if (j0 + 2 * KT < kend) load(j0 + 2 * KT);
+    if constexpr (!RES) {
+      if (j0 + KT < kend) stage((it + 1) & 1);
+      __syncthreads();
+      if (j0 + 2 * KT < kend) load(j0 + 2 * KT);
+    }
   }
 
   // ---- normalise, store O[q][h*d + e] (runs of 4 consecutive e per lane)
@@ -774,17 +794,19 @@ __global__ __launch_bounds__(256, (attn3_occ<D, KT>())) void attn3_kernel(AttnAr
     l = lsum + xlane32(lsum);
   }
   const float inv = l > 0.f ? 1.f / l : 0.f;
-  if (qrow >= a.Lq) return;
-  T* __restrict__ O = (T*)a.o + (long)b * a.so + (long)h * (a.hso ? a.hso : D) + (long)qrow * a.ldo;
+  if (qrow < a.Lq) {
+    T* __restrict__ O = (T*)a.o + (long)b * a.so + (long)h * (a.hso ? a.hso : D) + (long)qrow * a.ldo;
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
+    for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = 32 * dt + 8 * k + 4 * hh;
-      if (e >= D) continue;
-      *(uint2*)(O + e) = make_uint2(Mfma<T>::pack2(oacc[dt][4 * k] * inv, oacc[dt][4 * k + 1] * inv),
-                                    Mfma<T>::pack2(oacc[dt][4 * k + 2] * inv, oacc[dt][4 * k + 3] * inv));
-    }
+      for (int k = 0; k < 4; ++k) {
+        const int e = 32 * dt + 8 * k + 4 * hh;
+        if (e >= D) continue;
+        *(uint2*)(O + e) = make_uint2(Mfma<T>::pack2(oacc[dt][4 * k] * inv, oacc[dt][4 * k + 1] * inv),
+                                      Mfma<T>::pack2(oacc[dt][4 * k + 2] * inv, oacc[dt][4 * k + 3] * inv));
+      }
+  }
+  }   // rep
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -947,11 +969,16 @@ void launchw(const AttnArgs& a, hipStream_t s) {
 
 template <typename T, int D, int KT, bool CAUSAL>
 void launch3_cfg(const AttnArgs& a, hipStream_t s) {
-  const int nq = (a.Lq + 127) / 128;
+  // query groups per block against resident K/V (cross-attention, Lk <= 2 KT): as many as keep >= 1024 blocks
+  const bool res = !CAUSAL && a.Lk <= 2 * KT && g_attn_qrep;
+  int qrep = 1;
+  if (res)
+    while (qrep < 8 && ((a.Lq + 128 * 2 * qrep - 1) / (128 * 2 * qrep)) * a.H * a.B >= 1024) qrep *= 2;
+  const int nq = (a.Lq + 128 * qrep - 1) / (128 * qrep);
   dim3 grid(nq * a.H * a.B), block(256);
   ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn3_kernel<") +
                                (std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short") + ", " +
-                               std::to_string(D) + ", " + std::to_string(KT) + ", " + (CAUSAL ? "true" : "false") + ">" +
+                               std::to_string(D) + ", " + std::to_string(KT) + ", " + (CAUSAL ? "true" : "false") + (res ? ", true" : ", false") + ">" +
                                (g_prof_shapes ? " [B " + std::to_string(a.B) + " Lq " + std::to_string(a.Lq) + " Lk " +
                                                     std::to_string(a.Lk) + "]"
                                               : std::string())
@@ -960,7 +987,15 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
   AttnArgs b = a;
   b.xcd = g_attn_xcd;
   b.prio = g_attn_prio;
-  attn3_kernel<T, D, KT, CAUSAL><<<grid, block, 0, s>>>(b);
+  b.qrep = qrep;
+  if constexpr (!CAUSAL) {
+    if (res) {
+      attn3_kernel<T, D, KT, false, true><<<grid, block, 0, s>>>(b);
+      IRX_LAUNCH_CHECK();
+      return;
+    }
+  }
+  attn3_kernel<T, D, KT, CAUSAL, false><<<grid, block, 0, s>>>(b);
   IRX_LAUNCH_CHECK();
 }
 
@@ -1053,7 +1088,8 @@ void attention(const AttnArgs& a, hipStream_t s) {
 }
 int g_attn_v3 = 1;
 int g_attn_xcd = 1;
-int g_attn_prio = 0;   // irx_set_option("attn_prio", 1): MFMA chains of attn3 at raised wave priority (A/B)
+int g_attn_prio = 0;
+int g_attn_qrep = 1;   // irx_set_option("attn_qrep", 0): one query group per block in cross-attention (A/B)   // irx_set_option("attn_prio", 1): MFMA chains of attn3 at raised wave priority (A/B)
 int g_attn_hm = 1;
 
 bool g_attn_v2 = true;

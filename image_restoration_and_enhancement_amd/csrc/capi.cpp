@@ -81,6 +81,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gemm_nmajor") g_gemm_nmajor = value;
   else if (n == "prof_shapes") g_prof_shapes = value;
   else if (n == "attn_prio") g_attn_prio = value;
+  else if (n == "attn_qrep") g_attn_qrep = value;
   else if (n == "op_imgs") g_op_imgs = value;
   else if (n == "gemm_sk_blocks") g_gemm_sk_blocks = value;
   else if (n == "vae_attn_rows") g_vae_attn_rows = value;

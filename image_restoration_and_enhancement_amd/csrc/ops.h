@@ -146,11 +146,13 @@ struct AttnArgs {
   int q_scaled = 0;       // q already multiplied by scale * log2(e) (folded into the to_q weights)
   int xcd = 0;            // (set by the launcher) XCD-grouped block order
   int prio = 0;           // (set by the launcher) s_setprio around the MFMA chains
+  int qrep = 1;           // (set by the launcher) query groups per block over resident K/V
 };
 void attention(const AttnArgs& a, hipStream_t s);
 extern bool g_attn_v2;
 extern int g_attn_v3;    // 32x32x16 kernel for bf16 / fp16 (0: the round-1 kernels, bf16 only)
 extern int g_attn_prio;
+extern int g_attn_qrep;
 extern int g_attn_xcd;   // 1: (batch, head) groups of q-blocks kept on one XCD (K/V shared in its L2)
 extern int g_attn_hm;    // 1: the UNet's q|k|v projections write head-major attention operands
 extern int g_attn_d40;   // bf16: 16x16x32 kernel (irx_set_option("attn_v2", 0) selects the 16x16x16 one)

@@ -616,6 +616,26 @@ def test_attention_v3_vs_v2_and_head_major(device, dt, B, Lq, Lk, C, heads):
     assert O.rel_err(got, ref) < 2 * TOL[dt]
 
 
+@pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("B,Lq,Lk,C", [(16, 4096, 77, 320), (16, 3600, 77, 320), (16, 4000, 128, 320),
+                                       (16, 2048, 20, 640), (32, 1024, 77, 1280)])
+def test_attention_resident_kv(device, dt, B, Lq, Lk, C):
+    """Cross-attention with K/V resident in LDS (Lk <= 128; qrep query groups per block, some blocks' last
+    groups entirely past Lq) equals the streamed attn3 kernel (irx_set_option("attn_qrep", 0)) bit for bit."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    q, k, v = _r(B, Lq, C, seed=66), _r(B, Lk, C, seed=67), _r(B, Lk, C, seed=68)
+    qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
+    got = O.attention(qd, kd, vd, 8)
+    L.call("irx_set_option", b"attn_qrep", 0)
+    try:
+        want = O.attention(qd, kd, vd, 8)
+    finally:
+        L.call("irx_set_option", b"attn_qrep", 1)
+    assert torch.equal(got, want)
+    ref = O.ref_attention(_q(q[:2], dt), _q(k[:2], dt), _q(v[:2], dt), 8)
+    assert O.rel_err(got[:2], ref) < 2 * TOL[dt]
+
+
 def _with_sk(v, fn):
     # v = 3: every K = 320 shape on gemm_sk (the default takes only the GEGLU projection there)
     from image_restoration_and_enhancement_amd import _lib as L
