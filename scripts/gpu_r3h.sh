@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT}"
 export TMPDIR=/tmp
-O=gpurun_out/r3final2; mkdir -p $O
+O=gpurun_out/r3final3; mkdir -p $O
 timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log; grep -E "FAILED" $O/tests.log | head -20
 if [ $rc -gt 1 ]; then exit $rc; fi
