@@ -69,6 +69,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--match", default="", help="only shapes whose label contains this")
     ap.add_argument("--ref", action="store_true", help="also time torch (hipBLASLt / MIOpen) on the same shapes")
     ap.add_argument("--variants", default="s2,ring64,small")
     args = ap.parse_args()
@@ -77,11 +78,14 @@ def main():
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
     base = {"large_tiles": 1, "gemm_deep": 0, "gemm_small": 0, "tile_256x320": 1, "splitk_inkernel": 1, "halo_pipe": 1,
-            "gemm_pp": 0}
+            "gemm_pp": 0, "gemm_force": 0}
     allv = {"s2": {}, "ring64": {"gemm_deep": 2}, "ring32": {"gemm_deep": 1}, "small": {"gemm_small": 1}, "4wave": {"large_tiles": 0},
             "no320": {"tile_256x320": 0}, "redk": {"splitk_inkernel": 0}, "no320redk": {"tile_256x320": 0, "splitk_inkernel": 0},
             "halo1": {"halo_pipe": 0}, "halo2": {"halo_pipe": 1}, "pp0": {"gemm_pp": 0}, "pp1": {"gemm_pp": 1},
-            "nm0": {"gemm_nmajor": 0}, "nm1": {"gemm_nmajor": 1}, "nm2": {"gemm_nmajor": 2}}
+            "nm0": {"gemm_nmajor": 0},
+            # forced tile / split (gemm_force = BM*100000 + BN*100 + splits): the 8x8-level split-K sweep
+            **{f"f{bm}x{bn}s{sp}": {"gemm_force": bm * 100000 + bn * 100 + sp}
+               for bm in (256, 128) for bn in (320, 256, 128) for sp in (1, 2, 4, 8)}, "nm1": {"gemm_nmajor": 1}, "nm2": {"gemm_nmajor": 2}}
     variants = [(v, allv[v]) for v in args.variants.split(",")]
 
     def setv(opts):
@@ -89,6 +93,8 @@ def main():
             L.call("irx_set_option", k.encode(), v)
     if args.only in ("", "conv"):
         for lab, N, H, W, C0, C1, Co, k, s, up in CONVS:
+            if args.match not in lab:
+                continue
             x0 = torch.randn(N, H, W, C0, device=dev, generator=g).to(dt)
             x1 = torch.randn(N, H, W, C1, device=dev, generator=g).to(dt) if C1 else None
             w = (torch.randn(Co, C0 + C1, k, k, device=dev, generator=g) / math.sqrt((C0 + C1) * k * k)).to(dt)
