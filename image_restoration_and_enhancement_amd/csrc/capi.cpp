@@ -68,6 +68,7 @@ int irx_set_option(const char* name, int value) {
   else if (n == "gemm_deep") g_gemm_deep = value;
   else if (n == "gemm_dbg") g_gemm_dbg = value;
   else if (n == "gn_v2") g_gn_v2 = value != 0;
+  else if (n == "ln_stats8") g_ln_stats8 = value;
   else if (n == "gn_fuse") g_gn_fuse = value;
   else if (n == "gn_parts") g_gn_parts = value;
   else if (n == "halo_split") g_halo_split = value;
