@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r3v; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_ln_fold_gpu.py -x -v --timeout 200 --timeout-method thread -m gpu > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
+timeout -k 10 400 python -u -m pytest -p tests.conftest scripts/scratch_ln_stats8.py -k stats8 -x -v --timeout 200 --timeout-method thread -m gpu > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
 tail -2 $O/tests.txt
 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --opt ln_stats8=1 > $O/bench_s1.txt 2>&1 || { tail -20 $O/bench_s1.txt; exit 1; }
 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_s0.txt 2>&1 || exit 1
