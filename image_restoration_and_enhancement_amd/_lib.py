@@ -17,6 +17,7 @@ IRX_MODEL_UNET, IRX_MODEL_VAE, IRX_MODEL_CLIP = 0, 1, 2
 IRX_LAYOUT_VEC, IRX_LAYOUT_MAT, IRX_LAYOUT_CONV, IRX_LAYOUT_EMB = 0, 1, 2, 3
 IRX_LAYOUT_MAT_GEGLU64, IRX_LAYOUT_VEC_GEGLU64 = 4, 5
 IRX_LAYOUT_VEC_LN_U, IRX_LAYOUT_VEC_LN_V = 6, 7
+IRX_RCCL_ID_BYTES = 128   # include/irx.h (sizeof(ncclUniqueId))
 
 
 class IrxError(RuntimeError):
@@ -62,6 +63,8 @@ _SIGS = {
     "irx_last_error": (C.c_char_p, []),
     "irx_version": (i32, []),
     "irx_set_option": (i32, [C.c_char_p, i32]),
+    "irx_get_option": (i32, [C.c_char_p, C.POINTER(i32)]),
+    "irx_option_name": (C.c_char_p, [i32]),
     "irx_profile_begin": (i32, []),
     "irx_graph_begin": (i32, [vp]),
     "irx_graph_end": (i32, [vp, C.POINTER(vp)]),
@@ -158,6 +161,43 @@ def call(name: str, *args):
     if _SIGS[name][0] is i32 and name not in ("irx_version", "irx_rccl_available") and rc != 0:
         raise IrxError(f"{name}: {lib.irx_last_error().decode(errors='replace')}")
     return rc
+
+
+def get_option(name: str) -> int:
+    v = C.c_int()
+    call("irx_get_option", name.encode(), C.byref(v))
+    return v.value
+
+
+def options() -> dict:
+    """Every runtime option and its current value."""
+    lib = load()
+    out, i = {}, 0
+    while True:
+        n = lib.irx_option_name(i)
+        if not n:
+            return out
+        out[n.decode()] = get_option(n.decode())
+        i += 1
+
+
+class option:
+    """Context manager: set runtime options (irx_set_option) for a block, restoring the previous values after."""
+
+    def __init__(self, **opts):
+        self.opts = opts
+        self.saved = {}
+
+    def __enter__(self):
+        for k, v in self.opts.items():
+            self.saved[k] = get_option(k)
+            call("irx_set_option", k.encode(), int(v))
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            call("irx_set_option", k.encode(), v)
+        return False
 
 
 def profile_begin() -> None:

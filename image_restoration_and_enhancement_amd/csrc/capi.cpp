@@ -59,48 +59,74 @@ extern "C" {
 const char* irx_last_error(void) { return last_error(); }
 int irx_version(void) { return 1; }
 
+// every runtime option by name: an int or a bool global (irx_set_option / irx_get_option)
+struct OptRef {
+  int* i = nullptr;
+  bool* b = nullptr;
+};
+static const struct { const char* name; int* i; bool* b; } kOpts[] = {
+    {"large_tiles", nullptr, &g_large_tiles},
+    {"attn_v2", nullptr, &g_attn_v2},
+    {"gemm_deep", &g_gemm_deep, nullptr},
+    {"gemm_dbg", &g_gemm_dbg, nullptr},
+    {"gn_v2", nullptr, &g_gn_v2},
+    {"ln_stats8", &g_ln_stats8, nullptr},
+    {"gn_fuse", &g_gn_fuse, nullptr},
+    {"gn_parts", &g_gn_parts, nullptr},
+    {"halo_split", &g_halo_split, nullptr},
+    {"halo_pipe", &g_halo_pipe, nullptr},
+    {"gemm_pp", &g_gemm_pp, nullptr},
+    {"ln_fold", &g_ln_fold, nullptr},
+    {"gemm_sk", &g_gemm_sk, nullptr},
+    {"large_mask", &g_large_mask, nullptr},
+    {"large_dense", &g_large_dense, nullptr},
+    {"arena_guard", &g_arena_guard, nullptr},
+    {"gemm_nmajor", &g_gemm_nmajor, nullptr},
+    {"prof_shapes", &g_prof_shapes, nullptr},
+    {"attn_prio", &g_attn_prio, nullptr},
+    {"attn_qrep", &g_attn_qrep, nullptr},
+    {"op_imgs", &g_op_imgs, nullptr},
+    {"gemm_sk_blocks", &g_gemm_sk_blocks, nullptr},
+    {"vae_attn_rows", &g_vae_attn_rows, nullptr},
+    {"vae_flash", &g_vae_flash, nullptr},
+    {"splitk_inkernel", nullptr, &g_splitk_inkernel},
+    {"tile_256x320", nullptr, &g_tile_256x320},
+    {"gemm_force", &g_gemm_force, nullptr},
+    {"conv_halo", &g_conv_halo, nullptr},
+    {"gemm_small", nullptr, &g_gemm_small},
+    {"attn_d40", &g_attn_d40, nullptr},
+    {"attn_v3", &g_attn_v3, nullptr},
+    {"attn_xcd", &g_attn_xcd, nullptr},
+    {"attn_hm", &g_attn_hm, nullptr},
+    {"gemm_small_kmax", &g_gemm_small_kmax, nullptr},
+    {"nlm_strip", &g_nlm_strip, nullptr},
+    {"nlm_v2", &g_nlm_v2, nullptr},
+    {"nlm2_strip", &g_nlm2_strip, nullptr},
+};
+static OptRef opt_ref(const std::string& n) {
+  for (const auto& o : kOpts)
+    if (n == o.name) return {o.i, o.b};
+  throw Error("unknown option " + n);
+}
+
 int irx_set_option(const char* name, int value) {
   IRX_API_BEGIN
   IRX_CHECK(name, "null option name");
-  const std::string n(name);
-  if (n == "large_tiles") g_large_tiles = value != 0;
-  else if (n == "attn_v2") g_attn_v2 = value != 0;
-  else if (n == "gemm_deep") g_gemm_deep = value;
-  else if (n == "gemm_dbg") g_gemm_dbg = value;
-  else if (n == "gn_v2") g_gn_v2 = value != 0;
-  else if (n == "ln_stats8") g_ln_stats8 = value;
-  else if (n == "gn_fuse") g_gn_fuse = value;
-  else if (n == "gn_parts") g_gn_parts = value;
-  else if (n == "halo_split") g_halo_split = value;
-  else if (n == "halo_pipe") g_halo_pipe = value;
-  else if (n == "gemm_pp") g_gemm_pp = value;
-  else if (n == "ln_fold") g_ln_fold = value;
-  else if (n == "gemm_sk") g_gemm_sk = value;
-  else if (n == "large_mask") g_large_mask = value;
-  else if (n == "large_dense") g_large_dense = value;
-  else if (n == "arena_guard") g_arena_guard = value;
-  else if (n == "gemm_nmajor") g_gemm_nmajor = value;
-  else if (n == "prof_shapes") g_prof_shapes = value;
-  else if (n == "attn_prio") g_attn_prio = value;
-  else if (n == "attn_qrep") g_attn_qrep = value;
-  else if (n == "op_imgs") g_op_imgs = value;
-  else if (n == "gemm_sk_blocks") g_gemm_sk_blocks = value;
-  else if (n == "vae_attn_rows") g_vae_attn_rows = value;
-  else if (n == "vae_flash") g_vae_flash = value;
-  else if (n == "splitk_inkernel") g_splitk_inkernel = value != 0;
-  else if (n == "tile_256x320") g_tile_256x320 = value != 0;
-  else if (n == "gemm_force") g_gemm_force = value;
-  else if (n == "conv_halo") g_conv_halo = value;
-  else if (n == "gemm_small") g_gemm_small = value != 0;
-  else if (n == "attn_d40") g_attn_d40 = value;
-  else if (n == "attn_v3") g_attn_v3 = value;
-  else if (n == "attn_xcd") g_attn_xcd = value;
-  else if (n == "attn_hm") g_attn_hm = value;
-  else if (n == "gemm_small_kmax") g_gemm_small_kmax = value;
-  else if (n == "nlm_strip") g_nlm_strip = value;
-  else if (n == "nlm_v2") g_nlm_v2 = value;
-  else if (n == "nlm2_strip") g_nlm2_strip = value;
-  else throw Error("unknown option " + n);
+  const OptRef r = opt_ref(name);
+  if (r.i) *r.i = value;
+  else *r.b = value != 0;
+  IRX_API_END
+}
+
+const char* irx_option_name(int i) {
+  return i >= 0 && i < (int)(sizeof(kOpts) / sizeof(kOpts[0])) ? kOpts[i].name : nullptr;
+}
+
+int irx_get_option(const char* name, int* value) {
+  IRX_API_BEGIN
+  IRX_CHECK(name && value, "null argument");
+  const OptRef r = opt_ref(name);
+  *value = r.i ? *r.i : (*r.b ? 1 : 0);
   IRX_API_END
 }
 

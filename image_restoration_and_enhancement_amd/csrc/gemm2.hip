@@ -290,6 +290,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       bro[j] = n0 + r < a.N ? Bp + (long)(n0 + r) * a.ldb + (((lane % CPR) ^ swz(r)) * 8) : nullptr;
     }
     auto issueB = [&](int kt) {   // group 1: all of B(kt)
+      if (a.dbg & 4) return;      // (timing diagnostics: no B DMA)
       const int c = kt / 9, t = kt - 9 * c;
       const int off = t * Cin + c * BK;
       uint4* const st = Bsm + (kt % S) * BN * CPR;
@@ -300,6 +301,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       }
     };
     auto issueH = [&](int c, int j0, int j1) {   // group 0: pieces [j0, j1) of slab c's halo
+      if (a.dbg & 8) return;      // (timing diagnostics: no halo DMA)
       const bool second = c * BK >= a.g.C0;
       const uint16_t* sb = second ? (const uint16_t*)a.g.src1 : (const uint16_t*)a.g.src0;
       const int cs = second ? a.g.C1 : a.g.C0;
@@ -339,6 +341,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     uint4 fa[KSUB][TM], fb[KSUB][TN];
     auto readF = [&](auto tc, const uint4* Hs) {   // this wave's fragments of tap t (both 32-deep sub-steps)
       constexpr int t = decltype(tc)::value, ky = t / 3, kx = t % 3, st = t % S;
+      if (a.dbg & 16) return;     // (timing diagnostics: no fragment reads)
       const uint4* Bs = Bsm + st * BN * CPR + bwave;
       const uint4* Hrow = Hs + awave + ky * rowW + (kx - 1) * CPR;
 #pragma unroll
@@ -363,7 +366,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[ss][i], fb[ss][j], acc[i][j]);
     };
-    auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    const bool nobar = (a.dbg & 32) != 0;   // (timing diagnostics: no barriers)
+    auto barrier = [&] {
+      if (nobar) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
     // this split's K steps [kt0, nk): whole slabs (host: sp.per is a multiple of 9); >= 9 steps per split
     const int nk = kt1, c0 = kt0 / 9, cend = (kt1 + 8) / 9;
     if (g1) {

@@ -93,9 +93,10 @@ constexpr int kSkRC = kSkK / 8;    // 16-byte chunks per A row
 //
 // Every global -> LDS transfer is LDS-DMA issued from inline asm and every wait on it an explicit, exactly counted
 // vmcnt (the loop issues no compiler-visible load, so the compiler adds no wait of its own that would also drain the
-// DMA in flight).  Rows past M in the last tile are bound to tile row (r & 1): they re-read that row's A, residual and
-// LayerNorm statistics, and their store rewrites that row with identical bytes — every DMA and store is issued by
-// every wave, so the counts hold for ragged M too (M even; the host checks it when the statistics are read).
+// DMA in flight).  Rows past M in the last tile are bound to a valid tile row (`spare`: r & 1, or row 0 when the tile
+// has a single valid row): they re-read that row's A, residual and LayerNorm statistics, and their store rewrites that
+// row with identical bytes — every DMA and store is issued by every wave, so the counts hold for ragged M too (M even
+// when the statistics are read: they travel as row pairs; the host checks it).
 template <typename T, int NB, bool GEGLU, int MB, int BPC, bool RES, int S, bool AF2>
 __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_slices, int groups) {
   constexpr int BM = 16 * MB, KS = kSkKS, RC = kSkRC;
@@ -124,6 +125,8 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // tile row r, or the valid row that stands in for it when r is past M (rem >= 1 valid rows in the tile)
+  auto spare = [](int r, int rem) { return r < rem ? r : (rem > 1 ? (r & 1) : 0); };
   const int x = blockIdx.x & 7, loc = blockIdx.x >> 3;
   const int sl = loc % n_slices, grp = loc / n_slices;
   if (grp >= groups) return;
@@ -189,7 +192,7 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
     for (int j = 0; j < PPW; ++j) {
       const int p = (w * PPW + j) * 64 + lane;
       const int r = p / RC, c = (p % RC) ^ (r & 7);
-      glds16(base + (r < rem ? r : (r & 1)) * a.lda + c * 8, lds32(st + j * 64));
+      glds16(base + spare(r, rem) * a.lda + c * 8, lds32(st + j * 64));
     }
     if (has_ln) {
       if (lane < LNL) {
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
 #pragma unroll
       for (int k = 0; k < RESN; ++k) {
         const int p = lane + 64 * k, r = p / CH, c = p % CH;
-        glds16(R + (r < rem ? r : (r & 1)) * a.ldr + c * 8, lds32(dst + 64 * k));
+        glds16(R + spare(r, rem) * a.ldr + c * 8, lds32(dst + 64 * k));
       }
     }
   };
@@ -358,7 +361,7 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
           }
         }
         const int row = rr * 32 + crow(k);
-        const int srow2 = row < rem ? row : (row & 1);   // rows past M rewrite row (r & 1) with its own bytes
+        const int srow2 = spare(row, rem);               // rows past M rewrite their stand-in row with its own bytes
         *(uint4*)(Cp + mbase + srow2 * rstride + ncol[cch(k)]) = u;
       }
     }

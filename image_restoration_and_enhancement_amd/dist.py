@@ -52,27 +52,61 @@ def broadcast_blobs(blobs: Dict[str, torch.Tensor], src: int = 0) -> Dict[str, t
     return blobs
 
 
+def _all_ok(flag: bool) -> bool:
+    """True on every rank iff `flag` is true on every rank (one small object all-gather: works on any backend)."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return bool(flag)
+    flags = [None] * dist.get_world_size()
+    dist.all_gather_object(flags, bool(flag))
+    return all(flags)
+
+
 def rccl_comm(rank: int, world: int) -> C.c_void_p:
     """The engine's own RCCL communicator on the current HIP device (irx_rccl_comm_init through the C ABI).
-    Rank 0 makes the 128-byte unique id; it reaches the other ranks over the torch.distributed rendezvous
-    (host plumbing only — the collectives themselves are RCCL calls inside libirx)."""
+
+    Every rank takes the same branch, so no rank can be left waiting in a collective the others skipped:
+      1. each rank checks that librccl loads (irx_rccl_available); the flag is agreed across ranks first;
+      2. rank 0 makes the 128-byte unique id and ALWAYS enters the object broadcast — with the id, or with its
+         error text in place of it, which every rank then raises;
+      3. after ncclCommInitRank every rank reports success; if any rank failed, the ranks that did get a
+         communicator destroy it and all of them raise.
+    The id travels over the torch.distributed rendezvous (host plumbing only — the collectives themselves are
+    RCCL calls inside libirx).  Raises IrxError on every rank, or on none."""
     from . import _lib as L
-    idb = C.create_string_buffer(128)
+    if not _all_ok(L.call("irx_rccl_available") == 1):
+        raise L.IrxError("librccl cannot be loaded on every rank")
+    idb = C.create_string_buffer(L.IRX_RCCL_ID_BYTES)
+    err = ""
     if rank == 0:
-        L.call("irx_rccl_unique_id", idb)
-    obj = [idb.raw]
+        try:
+            L.call("irx_rccl_unique_id", idb)
+        except L.IrxError as e:
+            err = str(e) or "irx_rccl_unique_id failed"
+    obj = [(idb.raw, err)]
     if world > 1:
         dist.broadcast_object_list(obj, src=0)
+    uid, err0 = obj[0]
+    if err0:
+        raise L.IrxError(f"rank 0 could not make an RCCL unique id: {err0}")
     comm = C.c_void_p()
-    L.call("irx_rccl_comm_init", obj[0], world, rank, C.byref(comm))
+    err = ""
+    try:
+        L.call("irx_rccl_comm_init", uid, world, rank, C.byref(comm))
+    except L.IrxError as e:
+        err = str(e) or "irx_rccl_comm_init failed"
+    if not _all_ok(not err):
+        if not err:
+            L.call("irx_rccl_comm_destroy", comm)
+        raise L.IrxError(f"RCCL communicator init failed on some rank ({err or 'this rank ok'})")
     return comm
 
 
 def broadcast_models(models: Dict[str, object], src: int = 0) -> str:
     """Broadcast every model's bound weight blob from `src` with irx_weights_bcast (RCCL over xGMI, in place,
     on the current stream), name order.  Every rank must have bound a blob of the model's size.  Returns how
-    the weights moved: "none" (one rank), "irx_rccl", or — when the engine's RCCL cannot be initialised — the
-    torch.distributed broadcast of the same blobs, logged loudly and named in the return value."""
+    the weights moved: "none" (one rank), "irx_rccl", or — when the engine's RCCL cannot be initialised on
+    some rank — the torch.distributed broadcast of the same blobs, logged loudly and named in the return
+    value.  The choice is agreed across ranks (rccl_comm raises on all of them or on none)."""
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return "none"
     import torch
@@ -85,11 +119,12 @@ def broadcast_models(models: Dict[str, object], src: int = 0) -> str:
               file=sys.stderr, flush=True)
         broadcast_blobs({k: m.blob for k, m in models.items()}, src)
         return f"torch.distributed ({e})"
-    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream) if torch.cuda.is_available() else C.c_void_p()
     try:
         for k in sorted(models):
             L.call("irx_weights_bcast", models[k].h, comm, src, s)
-        torch.cuda.current_stream().synchronize()
+        if torch.cuda.is_available():
+            torch.cuda.current_stream().synchronize()
     finally:
         L.call("irx_rccl_comm_destroy", comm)
     return "irx_rccl"

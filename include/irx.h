@@ -90,6 +90,8 @@ int irx_version(void);
 
 /* engine options: "large_tiles" (1 = 8-wave LDS-DMA GEMM/conv path where eligible, 0 = 4-wave kernel) */
 int irx_set_option(const char* name, int value);
+int irx_get_option(const char* name, int* value);   /* current value of a runtime option (tests save / restore) */
+const char* irx_option_name(int i);                 /* i-th option name, NULL past the last */
 
 /* ---- optional per-launch HIP-event timing of the MFMA kernels (bench.py roofline) ---- */
 int irx_profile_begin(void);

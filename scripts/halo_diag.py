@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""What bounds the halo 3x3 conv (gemm2_kernel<256,160,...,HALO=2>)?  Times the UNet's halo-conv shapes (batch 16,
+512x512) with parts of the ping-pong main loop knocked out through the timing-diagnostic bits of option gemm_dbg
+(results are wrong when set): 2 no MFMAs, 4 no B DMA, 8 no halo DMA, 16 no fragment reads, 32 no barriers,
+1 no epilogue.  Variants interleave in one process (HIP events, median of rounds).
+  python scripts/halo_diag.py [--iters 20] [--rounds 3] [--dbg 0,1,2,4,8,16,32,36,44]"""
+from __future__ import annotations
+
+import argparse
+import math
+import statistics
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from image_restoration_and_enhancement_amd import _lib as L  # noqa: E402
+from tests import opref as O  # noqa: E402
+
+SHAPES = [  # (label, N, H, W, C0, C1, Cout)
+    ("conv320@64", 16, 64, 64, 320, 0, 320),
+    ("cat640+320->320@64", 16, 64, 64, 640, 320, 320),
+    ("conv640@32", 16, 32, 32, 640, 0, 640),
+    ("conv1280@16 (split 2)", 16, 16, 16, 1280, 0, 1280),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--dbg", default="0,1,2,4,8,12,16,32,20,36")
+    ap.add_argument("--opt", action="append", default=[])
+    a = ap.parse_args()
+    L.load()
+    for o in a.opt:
+        k, v = o.split("=")
+        L.call("irx_set_option", k.encode(), int(v))
+    dev, dt = torch.device("cuda"), torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    dbgs = [int(x) for x in a.dbg.split(",")]
+    for lab, N, H, W, C0, C1, Co in SHAPES:
+        x0 = torch.randn(N, H, W, C0, device=dev, generator=g).to(dt)
+        x1 = torch.randn(N, H, W, C1, device=dev, generator=g).to(dt) if C1 else None
+        wk = (torch.randn(Co, 3, 3, C0 + C1, device=dev, generator=g) / math.sqrt(9 * (C0 + C1))).to(dt)
+        b = torch.zeros(Co, device=dev)
+        out = torch.empty(N, H, W, Co, dtype=dt, device=dev)
+        flops = 2.0 * N * H * W * Co * (C0 + C1) * 9
+
+        def run():
+            L.call("irx_op_conv2d", O.S(), O.DT[dt], O.P(x0), O.P(x1), C0, C1, N, H, W, H, W, O.P(wk), O.P(b), Co,
+                   3, 3, 1, 1, 1, H, W, None, 0, None, O.P(out), 0, 0)
+        times = {d: [] for d in dbgs}
+        for _ in range(a.rounds):
+            for d in dbgs:
+                L.call("irx_set_option", b"gemm_dbg", d)
+                for _ in range(2):
+                    run()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    run()
+                e1.record()
+                torch.cuda.synchronize()
+                times[d].append(e0.elapsed_time(e1) / a.iters * 1e3)
+        L.call("irx_set_option", b"gemm_dbg", 0)
+        base = statistics.median(times[0])
+        print(f"{lab}: {flops / base / 1e6:.0f} TF/s at dbg 0", flush=True)
+        for d in dbgs:
+            us = statistics.median(times[d])
+            print(f"  dbg {d:3d}: {us:8.1f} us  ({us / base:5.2f} x)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

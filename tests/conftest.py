@@ -23,3 +23,17 @@ def device():
 
 
 REFERENCE = Path("/root/reference")
+
+
+@pytest.fixture(autouse=True)
+def _restore_options():
+    """Every test leaves the engine's runtime options (irx_set_option) as it found them: a snapshot before the test,
+    restored after it (a toggle restored to a non-default value changed what later tests ran)."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    before = L.options() if L._lib is not None else None
+    yield
+    if before is None or L._lib is None:
+        return
+    for k, v in L.options().items():
+        if before.get(k, v) != v:
+            L.call("irx_set_option", k.encode(), before[k])

@@ -14,7 +14,7 @@ inpaint_ref = :758-767) with the seeded random SD-1.5 weights (weights.random_st
   timesteps   int64 [n]         the executed grid
   fp_<model>  fp64 [2]          weights fingerprint (sum, sum |x|) of unet / vae / clip
 
-Usage:  python tests/golden/make_golden_e2e.py [--only cfg2_denoise_bf16] [--threads 8]
+Usage:  python tests/golden/make_golden_e2e.py [--only cfg2_denoise_bf16] [--threads 8] [--rows first|last|both]
 """
 from __future__ import annotations
 
@@ -34,13 +34,15 @@ from oracle import pipeline_ref as PR  # noqa: E402
 from tests import models_common as MC  # noqa: E402
 
 
-def run_case(name: str, c: dict):
+def run_case(name: str, c: dict, row: int = 0):
+    """Row `row` of the case's batch (image seed c["seed"] + row) through the oracle -> e2e_<name>.npz (row 0) or
+    e2e_<name>_last.npz (the batch's last row: the engine runs it at the end of the batch, off the row-tile start)."""
     task = c["task"]
     model_task = "inpaint" if task == "inpaint" else "denoise"
     prompt, strength, _, guidance = PR.TASKS[task]
     pc, sd = MC.state_dicts(model_task)
     models = MC.oracle_models(model_task)
-    imgs, masks = MC.task_images(task, c["res"], 1, c["seed"])
+    imgs, masks = MC.task_images(task, c["res"], 1, c["seed"] + row)
     ids_n = MC.prompt_ids("") if guidance > 1 else None
     t0 = time.perf_counter()
     with torch.no_grad():
@@ -53,26 +55,32 @@ def run_case(name: str, c: dict):
                                guidance, 42, c["sched"])
     dt = time.perf_counter() - t0
     out = {"image": np.asarray(r.image), "latents": r.latents[0].float().numpy(),
-           "timesteps": np.array(r.timesteps, np.int64), "cpu_seconds": np.array(dt)}
+           "timesteps": np.array(r.timesteps, np.int64), "cpu_seconds": np.array(dt), "row": np.array(row)}
     if c["dtype"] == "fp32":
         out["decoded16"] = np.round(r.decoded_float * 65535.0).astype(np.uint16)
     for k in ("unet", "vae", "clip"):
         out[f"fp_{k}"] = MC.weight_fingerprint(sd[k])
-    np.savez_compressed(HERE / f"e2e_{name}.npz", **out)
-    print(f"{name}: {len(r.timesteps)} evals, {dt:.0f} s", flush=True)
+    tag = name if row == 0 else f"{name}_last"
+    np.savez_compressed(HERE / f"e2e_{tag}.npz", **out)
+    print(f"{tag}: row {row}, {len(r.timesteps)} evals, {dt:.0f} s", flush=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", action="append", default=[])
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--rows", default="first", choices=["first", "last", "both"],
+                    help="first: row 0 (e2e_<case>.npz); last: the batch's last row (e2e_<case>_last.npz)")
     a = ap.parse_args()
     if a.threads:
         torch.set_num_threads(a.threads)
     for name, c in MC.E2E_CASES.items():
         if a.only and name not in a.only:
             continue
-        run_case(name, c)
+        if a.rows in ("first", "both"):
+            run_case(name, c)
+        if a.rows in ("last", "both") and c["batch"] > 1:
+            run_case(name, c, c["batch"] - 1)
 
 
 if __name__ == "__main__":

@@ -45,8 +45,9 @@ def conv2d(x0, w_oihw, bias, stride=1, pad=(1, 1), out_hw=None, x1=None, up_hw=N
     return out
 
 
-def gemm(A, Bw, bias=None, alpha=1.0, act=0, residual=None, out_f32=False, batch=1):
-    """A [M,K] (or [b,M,K]), Bw [N,K] (or [b,N,K]) device tensors -> [M,N]."""
+def gemm(A, Bw, bias=None, alpha=1.0, act=0, residual=None, out_f32=False, batch=1, guard_rows=0):
+    """A [M,K] (or [b,M,K]), Bw [N,K] (or [b,N,K]) device tensors -> [M,N].  guard_rows > 0: the output is the head
+    of a larger buffer whose trailing rows hold a sentinel, asserted untouched after the call (no write past M)."""
     dt = A.dtype
     if batch > 1:
         _, M, K = A.shape
@@ -56,6 +57,12 @@ def gemm(A, Bw, bias=None, alpha=1.0, act=0, residual=None, out_f32=False, batch
     else:
         M, K = A.shape
         N = Bw.shape[0]
+        if guard_rows:
+            buf = torch.full((M + guard_rows, N), 1234.0, dtype=torch.float32 if out_f32 else dt, device=A.device)
+            L.call("irx_op_gemm", S(), DT[dt], M, N, K, P(A), K, P(Bw), K, P(buf), N, P(bias), float(alpha), act,
+                   P(residual), N, int(out_f32), 1, 0, 0, 0, 0)
+            assert bool((buf[M:] == 1234.0).all()), "GEMM wrote past its last output row"
+            return buf[:M]
         out = torch.empty((M, N), dtype=torch.float32 if out_f32 else dt, device=A.device)
         sA = sB = sC = 0
     L.call("irx_op_gemm", S(), DT[dt], M, N, K, P(A), K, P(Bw), K, P(out), N, P(bias), float(alpha), act,

@@ -70,3 +70,92 @@ def test_gloo_world2_broadcast_gather_max():
         assert ok_b is True, ok_b
         assert ok_g is True
         assert mx == 2.5
+
+
+class _Model:
+    """Stand-in for a bound irx model: a handle and its packed weight blob."""
+
+    def __init__(self, h, blob):
+        self.h, self.blob = h, blob
+
+
+def _stub_lib(L, rank, scenario, models, log):
+    """_lib.call replaced by a stub: the RCCL entry points succeed or fail per `scenario`, and irx_weights_bcast
+    moves the blob with a gloo broadcast so the data path can be checked end to end on the CPU."""
+    import ctypes as C
+    import torch.distributed as dist
+    uid = bytes(range(128))
+
+    def call(name, *args):
+        log.append(name)
+        if name == "irx_rccl_available":
+            return 0 if (scenario == "nolib" and rank == 1) else 1
+        if name == "irx_rccl_unique_id":
+            if scenario == "noid":
+                raise L.IrxError("ncclGetUniqueId: stub failure")
+            C.memmove(args[0], uid, len(uid))
+            return 0
+        if name == "irx_rccl_comm_init":
+            idb, world, r, pcomm = args
+            assert bytes(idb)[:128] == uid and world == 2 and r == rank
+            if scenario == "initfail" and rank == 1:
+                raise L.IrxError("ncclCommInitRank: stub failure")
+            pcomm._obj.value = 1000 + rank
+            return 0
+        if name == "irx_rccl_comm_destroy":
+            assert args[0].value == 1000 + rank
+            return 0
+        if name == "irx_weights_bcast":
+            h, comm, src, _s = args
+            assert comm.value == 1000 + rank
+            dist.broadcast(next(m.blob for m in models.values() if m.h == h), src=src)
+            return 0
+        raise AssertionError(f"unexpected call {name}")
+    return call
+
+
+def _bcast_worker(rank, world, port, scenario, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        from image_restoration_and_enhancement_amd import _lib as L
+        D.init("gloo")
+        g = torch.Generator().manual_seed(7)
+        ref = {"unet": torch.randint(0, 256, (4096,), dtype=torch.uint8, generator=g),
+               "vae": torch.randint(0, 256, (513,), dtype=torch.uint8, generator=g)}
+        models = {k: _Model(i + 1, v.clone() if rank == 0 else torch.zeros_like(v)) for i, (k, v) in enumerate(ref.items())}
+        log = []
+        L.call = _stub_lib(L, rank, scenario, models, log)
+        how = D.broadcast_models(models)
+        ok = all(torch.equal(models[k].blob, ref[k]) for k in ref)
+        D.barrier()
+        q.put((rank, how.split(" ")[0], ok, log.count("irx_rccl_comm_destroy"), log.count("irx_weights_bcast")))
+    except Exception as ex:  # report instead of hanging the parent
+        q.put((rank, repr(ex), None, None, None))
+    finally:
+        if torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("scenario", ["ok", "nolib", "noid", "initfail"])
+def test_broadcast_models_rank_consistent(scenario):
+    """dist.broadcast_models with _lib.call stubbed: every rank takes the same path —
+    irx_weights_bcast when RCCL comes up everywhere, the torch.distributed broadcast on every rank when librccl is
+    missing on one rank, rank 0 cannot make the unique id, or one rank's communicator init fails (the ranks that got
+    a communicator destroy it) — and the blobs arrive intact either way."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, 2, port, scenario, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    want = "irx_rccl" if scenario == "ok" else "torch.distributed"
+    for rank, how, ok, destroyed, bcasts in res:
+        assert how == want, (rank, how)
+        assert ok is True
+        assert bcasts == (2 if scenario == "ok" else 0)
+        exp_destroy = 1 if scenario == "ok" or (scenario == "initfail" and rank == 0) else 0
+        assert destroyed == exp_destroy, (rank, destroyed)

@@ -1,8 +1,8 @@
 """Full-length end-to-end parity against committed oracle goldens (VERDICT r2 "next" #1).
 
 Each case of tests/models_common.E2E_CASES is a BASELINE.json config at its real step count: the per-GPU batch
-runs through the engine in the config's dtype, and row 0 is compared with the CPU fp32 oracle's output for the
-same image, weights and seed, generated once in the build container by tests/golden/make_golden_e2e.py
+runs through the engine in the config's dtype, and row 0 and the batch's last row are compared with the CPU fp32
+oracle's outputs for the same images, weights and seed (e2e_<case>.npz / e2e_<case>_last.npz), generated once in the build container by tests/golden/make_golden_e2e.py
 (oracle/pipeline_ref.py: the diffusers calls at src/inference.py:486-495, :566-573, :664-672, :758-767).
 The oracle does not run here: the goldens carry its outputs, and a weight fingerprint pins that this box
 regenerated exactly the seeded weights they were made with.
@@ -74,34 +74,45 @@ def run_case(device, name):
     assert got.timesteps == g["timesteps"].tolist()
     assert got.images_u8.shape[0] == c["batch"]
     assert torch.isfinite(got.latents).all() and torch.isfinite(got.decoded01).all()
-    dec = got.decoded01[0].cpu().numpy()
-    # fp32 cases carry the decoded floats (uint16 steps of 1/65535); 16-bit cases only the uint8 image, whose
-    # rounding (<= 0.5/255) is far inside their bars
-    ref_dec = (g["decoded16"].astype(np.float64) / 65535.0 if "decoded16" in g
-               else g["image"].astype(np.float64) / 255.0)
-    lat = got.latents[0].permute(2, 0, 1).cpu().numpy()           # NHWC -> [4, h, w]
-    m = {"max_abs": float(np.abs(dec - ref_dec).max()),
-         "u8_max": int(np.abs(got.images_u8[0].cpu().numpy().astype(int) - g["image"].astype(int)).max()),
-         "psnr": float(M.psnr(g["image"], got.images_u8[0].cpu().numpy())),
-         "ssim": float(M.ssim(g["image"], got.images_u8[0].cpu().numpy())),
-         "rel_l2": float(np.linalg.norm(dec - ref_dec) / np.linalg.norm(ref_dec)),
-         "lat_rel_l2": float(np.linalg.norm(lat - g["latents"]) / np.linalg.norm(g["latents"])),
-         "lat_rel_max": float(np.abs(lat - g["latents"]).max() / np.abs(g["latents"]).max()),
-         "evals": len(got.timesteps)}
-    print(f"\nE2E {name}: {m}")
-    return m
+
+    def metrics(row, g):
+        dec = got.decoded01[row].cpu().numpy()
+        # fp32 cases carry the decoded floats (uint16 steps of 1/65535); 16-bit cases only the uint8 image, whose
+        # rounding (<= 0.5/255) is far inside their bars
+        ref_dec = (g["decoded16"].astype(np.float64) / 65535.0 if "decoded16" in g
+                   else g["image"].astype(np.float64) / 255.0)
+        lat = got.latents[row].permute(2, 0, 1).cpu().numpy()           # NHWC -> [4, h, w]
+        img = got.images_u8[row].cpu().numpy()
+        return {"row": row, "max_abs": float(np.abs(dec - ref_dec).max()),
+                "u8_max": int(np.abs(img.astype(int) - g["image"].astype(int)).max()),
+                "psnr": float(M.psnr(g["image"], img)), "ssim": float(M.ssim(g["image"], img)),
+                "rel_l2": float(np.linalg.norm(dec - ref_dec) / np.linalg.norm(ref_dec)),
+                "lat_rel_l2": float(np.linalg.norm(lat - g["latents"]) / np.linalg.norm(g["latents"])),
+                "lat_rel_max": float(np.abs(lat - g["latents"]).max() / np.abs(g["latents"]).max()),
+                "evals": len(got.timesteps)}
+    ms = [metrics(0, g)]
+    if c["batch"] > 1:
+        # the batch's last row: its rows sit at the end of the batch, away from the row-tile starts
+        gl = _golden(f"{name}_last")
+        assert int(gl["row"]) == c["batch"] - 1 and gl["timesteps"].tolist() == got.timesteps
+        ms.append(metrics(c["batch"] - 1, gl))
+    for m in ms:
+        print(f"\nE2E {name}: {m}")
+    return ms
 
 
 def test_e2e_cfg1_fp32_full_pndm(device):
     """configs[0] (512x512 denoise, 20 PNDM steps x 0.5 = 11 evals, CFG 5.0) through the fp32 engine in full."""
-    m = run_case(device, "cfg1_denoise_fp32")
+    m, = run_case(device, "cfg1_denoise_fp32")
     assert m["evals"] == 11
     assert m["max_abs"] < 1e-3 and m["u8_max"] <= 1 and m["lat_rel_max"] < 1e-4, m
 
 
 @pytest.mark.parametrize("name", ["cfg2_denoise_bf16", "cfg3_sr_bf16", "cfg4_inpaint_bf16", "cfg5_colorize_fp16"])
 def test_e2e_16bit_full_length(device, name):
-    m = run_case(device, name)
+    ms = run_case(device, name)
     want = {"cfg2_denoise_bf16": 25, "cfg3_sr_bf16": 40, "cfg4_inpaint_bf16": 30, "cfg5_colorize_fp16": 37}[name]
-    assert m["evals"] == want
-    assert m["psnr"] >= PSNR_MIN[name] and m["rel_l2"] < REL_MAX[name] and m["lat_rel_l2"] < LAT_MAX[name], m
+    assert len(ms) == 2                 # row 0 and the last row, same bars
+    for m in ms:
+        assert m["evals"] == want
+        assert m["psnr"] >= PSNR_MIN[name] and m["rel_l2"] < REL_MAX[name] and m["lat_rel_l2"] < LAT_MAX[name], m

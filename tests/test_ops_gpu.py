@@ -507,7 +507,7 @@ def test_conv_halo_pipelined_bit_exact(device, case, dt):
 ])
 @pytest.mark.parametrize("dt", DT16)
 def test_gemm_pingpong_bit_exact(device, M, N, K, res, conv, dt):
-    """The ping-pong main loop (option gemm_pp, default) issues every accumulator's MFMAs in the round-2 order
+    """The ping-pong main loop (option gemm_pp; off by default, measured slower) issues every accumulator's MFMAs in the round-2 order
     (32-deep K sub-steps, ascending; the same split-K boundaries): outputs identical bit for bit."""
     from image_restoration_and_enhancement_amd import _lib as L
     from image_restoration_and_enhancement_amd.engine import geglu64_order
@@ -538,7 +538,7 @@ def test_gemm_pingpong_bit_exact(device, M, N, K, res, conv, dt):
         torch.cuda.synchronize()
         assert torch.equal(outs[0], outs[1])
     finally:
-        L.call("irx_set_option", b"gemm_pp", 1)
+        L.call("irx_set_option", b"gemm_pp", 0)
 
 
 @pytest.mark.parametrize("B,L", [(2, 256), (1, 333), (2, 1024), (1, 77)])
@@ -649,7 +649,9 @@ def _with_sk(v, fn):
 
 
 @pytest.mark.parametrize("M,N,res", [(5000, 320, True), (65536, 960, False), (777, 640, True), (64, 320, False),
-                                     (16384, 2560, False)])
+                                     (16384, 2560, False),
+                                     # M = 1 (mod the tile): a last tile with a single valid row
+                                     (1025, 320, True), (4097, 960, False), (65, 320, False)])
 @pytest.mark.parametrize("dt", DT16)
 def test_gemm_sk(device, M, N, res, dt):
     """K = 320 streaming kernel (gemm_sk.hip: B slice in registers, A ring, lane-local epilogue) vs fp32, and
@@ -660,7 +662,7 @@ def test_gemm_sk(device, M, N, res, dt):
     bias = _r(N, seed=92)
     R = _r(M, N, seed=93) if res else None
     a_d, b_d, r_d = _dev(A, dt, device), _dev(Bw, dt, device), (_dev(R, dt, device) if res else None)
-    run = lambda: O.gemm(a_d, b_d, bias=bias.to(device), residual=r_d)       # noqa: E731
+    run = lambda: O.gemm(a_d, b_d, bias=bias.to(device), residual=r_d, guard_rows=8)       # noqa: E731
     sk, lt = _with_sk(3, run), _with_sk(0, run)
     ref = _q(A, dt) @ _q(Bw, dt).T + bias + (_q(R, dt) if res else 0)
     assert O.rel_err(sk, ref) < TOL[dt]
@@ -679,7 +681,7 @@ def _same_as_large_tile(sk, lt, dt):
 
 
 @pytest.mark.parametrize("dt", DT16)
-@pytest.mark.parametrize("M", [8192, 1000])
+@pytest.mark.parametrize("M", [8192, 1000, 1025, 33])
 def test_gemm_sk_geglu(device, M, dt):
     """GEGLU feed-forward projection at K = 320 on the streaming kernel: vs fp32 and bit for bit vs the
     large-tile kernel's fused GEGLU epilogue."""
@@ -693,9 +695,11 @@ def test_gemm_sk_geglu(device, M, dt):
     a_d, w_d, b_d = _dev(A, dt, device), _dev(Wt[perm], dt, device), bias[perm].to(device).contiguous()
 
     def run():
-        out = torch.empty(M, 4 * C, dtype=dt, device=device)
-        L.call("irx_op_gemm_geglu", O.S(), O.DT[dt], M, 8 * C, C, O.P(a_d), O.P(w_d), O.P(b_d), O.P(out))
-        return out
+        buf = torch.full((M + 8, 4 * C), 1234.0, dtype=dt, device=device)   # 8 guard rows: no write past M
+        L.call("irx_op_gemm_geglu", O.S(), O.DT[dt], M, 8 * C, C, O.P(a_d), O.P(w_d), O.P(b_d), O.P(buf))
+        torch.cuda.synchronize()
+        assert bool((buf[M:] == 1234.0).all()), "GEGLU GEMM wrote past its last output row"
+        return buf[:M]
     sk, lt = _with_sk(1, run), _with_sk(0, run)
     pr = _q(A, dt) @ _q(Wt, dt).T + bias
     h, g = pr.chunk(2, dim=-1)
