@@ -73,6 +73,9 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"ln_stats8", &g_ln_stats8, nullptr},
     {"gn_fuse", &g_gn_fuse, nullptr},
     {"gn_parts", &g_gn_parts, nullptr},
+    {"ln_parts", &g_ln_parts, nullptr},
+    {"gn_fold", &g_gn_fold, nullptr},
+    {"geglu_partial", &g_geglu_partial, nullptr},
     {"halo_split", &g_halo_split, nullptr},
     {"halo_pipe", &g_halo_pipe, nullptr},
     {"gemm_pp", &g_gemm_pp, nullptr},
@@ -650,6 +653,40 @@ int irx_op_attention_hm(void* s, int dtype, int B, int H, int lq, int lk, int d,
   a.o = o; a.ldo = d; a.so = (long)H * lq * d; a.hso = (long)lq * d;
   a.scale = scale;
   attention(a, S(s));
+  IRX_API_END
+}
+
+int irx_op_gemm_ln_out(void* s, int dtype, int M, int N, int K, const void* A, const void* B, const float* bias,
+                       const void* residual, void* C, void* parts) {
+  IRX_API_BEGIN
+  GemmArgs a;
+  a.dtype = dtype; a.M = M; a.N = N; a.K = K;
+  a.A = A; a.lda = K; a.B = B; a.ldb = K;
+  a.C = C; a.ldc = N; a.bias = bias;
+  a.residual = residual; a.ldr = N;
+  a.imgs = g_op_imgs;
+  IRX_CHECK(parts && gemm_emits_ln_parts(a), "shape/dtype cannot emit LayerNorm partials");
+  a.ln_out = (float2*)parts;
+  gemm(a, S(s));
+  IRX_API_END
+}
+
+int irx_op_gemm_ln_fold(void* s, int dtype, int M, int N, int K, const void* A, const void* B, const float* u,
+                        const float* v, const void* rs, const void* parts, int T, int geglu, void* C) {
+  IRX_API_BEGIN
+  IRX_CHECK((rs != nullptr) != (parts != nullptr), "give the row statistics or the partials, not both");
+  GemmArgs a;
+  a.dtype = dtype; a.M = M; a.N = N; a.K = K;
+  a.A = A; a.lda = K; a.B = B; a.ldb = K;
+  a.C = C; a.ldc = geglu ? N / 2 : N; a.bias = v; a.geglu = geglu ? 1 : 0;
+  a.ln_u = u;
+  a.ln_rs = (const float2*)rs;
+  a.ln_part = (const float2*)parts;
+  a.ln_T = parts ? T : 0;
+  a.imgs = g_op_imgs;
+  IRX_CHECK(!geglu || gemm_geglu_fusable(a), "shape/dtype not eligible for the fused GEGLU epilogue");
+  IRX_CHECK(gemm_ln_foldable(a), "shape/dtype not eligible for the folded LayerNorm epilogue");
+  gemm(a, S(s));
   IRX_API_END
 }
 

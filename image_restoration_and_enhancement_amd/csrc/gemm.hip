@@ -280,13 +280,19 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   } else {
     IRX_CHECK(a.A && a.lda % vec == 0 && ((uintptr_t)a.A % 16) == 0, "A rows must be 16-byte aligned");
   }
-  IRX_CHECK(!a.ln_rs || (a.ln_u && gemm_ln_foldable(a)), "folded LayerNorm needs the large-tile path");
+  IRX_CHECK(!(a.ln_rs || a.ln_part) || (a.ln_u && gemm_ln_foldable(a)), "folded LayerNorm needs the large-tile path");
+  IRX_CHECK(!a.ln_part || (a.ln_T >= 1 && a.K == a.ln_T * kLnGroup), "LayerNorm partials must cover the K row");
   if (a.geglu) {
     IRX_CHECK(gemm_geglu_fusable(a) && gemm_large_tile(a, s), "GEGLU epilogue needs the large-tile path");
     return;
   }
-  if (a.ln_rs) {
+  if (a.ln_rs || a.ln_part) {
     IRX_CHECK(gemm_large_tile(a, s), "folded LayerNorm needs the large-tile path");
+    return;
+  }
+  if (a.ln_out || a.b_rows) {
+    IRX_CHECK((!a.ln_out || gemm_emits_ln_parts(a)) && (!a.b_rows || gemm_bimg_ok(a)) && gemm_large_tile(a, s),
+              "LayerNorm partials / per-image weights need the large-tile epilogue");
     return;
   }
   if (a.gn_part) {

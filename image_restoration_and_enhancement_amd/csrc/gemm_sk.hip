@@ -135,7 +135,8 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
   const int t0 = lo + grp;
   if (t0 >= hi) return;
   const int nt = (hi - t0 + groups - 1) / groups;   // tiles of this block: t0, t0 + groups, ...
-  const bool has_ln = !RES && a.ln_rs != nullptr;
+  const bool has_ln = !RES && (a.ln_rs != nullptr || a.ln_part != nullptr);
+  const float2* const lnsrc = a.ln_part ? a.ln_part : a.ln_rs;   // (ln_T == 1: one float2 per row either way)
   const int PA = PPW + (has_ln ? 1 : 0);            // A-tile DMA pieces per wave (+ the statistics piece)
 
   // weight row (index into B / bias / ln_u) of slice-local row idx
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
     if (has_ln) {
       if (lane < LNL) {
         const int r = 2 * (w * LNL + lane);   // rows r, r + 1 (M even: both valid or both past M)
-        glds16(a.ln_rs + m0 + (r < rem ? r : 0), lds32(lnring + (it % S) * BM + 2 * w * LNL));
+        glds16(lnsrc + m0 + (r < rem ? r : 0), lds32(lnring + (it % S) * BM + 2 * w * LNL));
       }
     }
   };
@@ -310,7 +311,11 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
 #pragma unroll
       for (int ih = 0; ih < 2; ++ih) {
         const int i = 2 * rr + ih;
-        const float2 rs = has_ln ? lst[i * 16 + (lane & 15)] : make_float2(1.f, 0.f);
+        float2 rs = has_ln ? lst[i * 16 + (lane & 15)] : make_float2(1.f, 0.f);
+        if (a.ln_part) {   // producer partial (mean, M2) -> (rstd, rstd * mean): ln_rs_at's arithmetic for one group
+          const float rstd = rsqrtf(rs.y / (float)kLnGroup + a.ln_eps);
+          rs = make_float2(rstd, rstd * rs.x);
+        }
         float v[NB][4];
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
@@ -395,14 +400,15 @@ void launch_sk(const GemmArgs& a, hipStream_t s) {
 // The decision depends only on the per-call shape (not on M), so it is the same for every batch size.
 bool gemm_sk_eligible(const GemmArgs& a) {
   if (!g_gemm_sk || (!a.geglu && g_gemm_sk != 3) || !is16(a.dtype) || a.conv || a.out_f32 || a.batch != 1 || a.K != kSkK) return false;
-  if (a.act != ACT_NONE || a.rowadd || a.gn_part || a.gn_ab) return false;
+  if (a.act != ACT_NONE || a.rowadd || a.gn_part || a.gn_ab || a.b_rows || a.ln_out) return false;
   if (a.geglu ? (a.N % 256 != 0 || a.N / 2 / 128 > 32 || a.residual || a.hs_L || a.ldc % 4) : (a.N % 320 || a.N / 320 > 32))
     return false;
   if (a.lda % 8 || a.ldb % 8 || ((uintptr_t)a.A % 16) || ((uintptr_t)a.B % 16)) return false;
   if (((uintptr_t)a.C % 8) || (a.hs_L ? (a.hs_d % 4 || a.hs_C % 4) : a.ldc % 4)) return false;
   if (a.residual && (a.ldr % 4 || ((uintptr_t)a.residual % 8))) return false;
   if (a.hs_L && (a.residual || a.hs_L % 64)) return false;   // (a 64-row tile lies in one image)
-  if (a.ln_rs && (a.alpha != 1.f || a.M % 2)) return false;   // (statistics DMA'd as row pairs)
+  if ((a.ln_rs || a.ln_part) && (a.alpha != 1.f || a.M % 2)) return false;   // (statistics DMA'd as row pairs)
+  if (a.ln_part && a.ln_T != 1) return false;   // (one producer partial per row: the K = 320 row)
   return a.M > 0;
 }
 

@@ -380,7 +380,7 @@ Act Unet::resnet(Ctx& c, const ResW& r, Act& x0, Act* x1, const float* tproj, fl
 }
 
 void Unet::ln_gemm(Ctx& c, GemmArgs& g, const void* x, int rows, int C, P lnw, P lnb, P u, P v, const float* bias,
-                   void* nbuf, float2* st) {
+                   void* nbuf, float2* st, const float2* parts) {
   g.lda = C;
   if (!ln_fold_) {
     lnorm(c, x, rows, C, lnw, lnb, 1e-5f, nbuf);
@@ -389,12 +389,19 @@ void Unet::ln_gemm(Ctx& c, GemmArgs& g, const void* x, int rows, int C, P lnw, P
   } else {
     g.bias = fptr(v);                 // bias + W beta
     g.A = x;
-    g.ln_rs = st;
     g.ln_u = fptr(u);
+    if (parts) {                      // statistics from the producer's partials: no pass over x
+      g.ln_part = parts;
+      g.ln_T = C / kLnGroup;
+      g.ln_eps = 1e-5f;
+    } else {
+      g.ln_rs = st;
+    }
     if (gemm_ln_foldable(g)) {
-      if (!c.ws->dry()) layer_norm_stats(dt_, x, C, rows, C, 1e-5f, st, c.s);
+      if (!parts && !c.ws->dry()) layer_norm_stats(dt_, x, C, rows, C, 1e-5f, st, c.s);
     } else {                          // (W * gamma, bias + W beta) after an affine-free LayerNorm
       g.ln_rs = nullptr;
+      g.ln_part = nullptr;
       g.ln_u = nullptr;
       if (!c.ws->dry()) layer_norm(dt_, x, C, rows, C, 1e-5f, nullptr, nullptr, nbuf, C, c.s);
       g.A = nbuf;
@@ -403,17 +410,67 @@ void Unet::ln_gemm(Ctx& c, GemmArgs& g, const void* x, int rows, int C, P lnw, P
   run_gemm(c, g);
 }
 
+const float2* Unet::xf_proj(Ctx& c, const void* A, int M, int C, P w, const float* bias, void* out,
+                            const void* residual, int imgs, float2* lnp) {
+  GemmArgs a;
+  a.dtype = dt_;
+  a.M = M; a.N = C; a.K = C;
+  a.A = A; a.lda = C;
+  a.B = ptr(w); a.ldb = C;
+  a.C = out; a.ldc = C;
+  a.bias = bias;
+  a.residual = residual; a.ldr = C;
+  a.imgs = imgs;
+  const bool emit = lnp && gemm_emits_ln_parts(a);   // (shape-only decision: the dry run decides the same)
+  if (emit) a.ln_out = lnp;
+  run_gemm(c, a);
+  return emit ? lnp : nullptr;
+}
+
 Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   const int B = x.n, HW = x.h * x.w, C = a.c;
   const long M = (long)B * HW;
   const size_t es = dsize(dt_);
   const int heads = cfg_.heads, d = C / heads;
   const float scale = 1.0f / std::sqrt((float)d);
-  Act gn = new_act(c, B, x.h, x.w, C);
-  gnorm(c, x, nullptr, a.nw, a.nb, 1e-6f, 0, gn);
   Act h = new_act(c, B, x.h, x.w, C);
-  linear(c, gn.p, C, M, C, a.piw, C, fptr(a.pib), h.p, C, ACT_NONE, nullptr, 0, 0, B);
-  drop(c, gn);
+  // LayerNorm partials of the residual stream h, emitted by the projections that write it (GemmArgs::ln_out)
+  float2* lnp = (ln_fold_ && C % kLnGroup == 0) ? (float2*)c.ws->alloc(M * (C / kLnGroup) * sizeof(float2)) : nullptr;
+  const float2* parts = nullptr;
+  // GroupNorm (no SiLU) -> proj_in: folded into per-image weights where they stay small next to the activation
+  // (C <= 640, i.e. the 64x64 / 32x32 levels): proj_in(GN(x)) = x (W diag(a_i))^T + (bias + W b_i) for image i with
+  // GN(x) = x * a_i + b_i per channel — the normalised tensor is neither written nor read
+  GemmArgs pg;
+  pg.dtype = dt_; pg.M = M; pg.N = C; pg.K = C;
+  pg.A = x.p; pg.lda = C; pg.ldb = C;
+  pg.C = h.p; pg.ldc = C;
+  pg.imgs = B;
+  pg.b_rows = HW; pg.b_img_stride = (long)C * C; pg.bias_img_stride = C;
+  pg.B = ptr(a.piw);   // (placeholder for the shape checks: the folded copies replace it below)
+  if (dt_ != F32 && g_gn_fold && C <= 640 && x.gnp && HW % x.gnr == 0 && gemm_bimg_ok(pg)) {
+    float2* ab = (float2*)c.ws->alloc((size_t)B * C * sizeof(float2));
+    void* wf = c.ws->alloc((size_t)B * C * C * es);
+    float* bf = (float*)c.ws->alloc((size_t)B * C * sizeof(float));
+    if (!c.ws->dry()) {
+      group_norm_parts_ab(C, B, HW, cfg_.norm_groups, 1e-6f, fptr(a.nw), fptr(a.nb), x.gnp, x.gnr, ab, c.s);
+      gn_fold_weights(dt_, ptr(a.piw), fptr(a.pib), ab, C, C, B, wf, bf, c.s);
+    }
+    pg.B = wf;
+    pg.bias = bf;
+    if (lnp && gemm_emits_ln_parts(pg)) {
+      pg.ln_out = lnp;
+      parts = lnp;
+    }
+    run_gemm(c, pg);
+    c.ws->free(bf);
+    c.ws->free(wf);
+    c.ws->free(ab);
+  } else {
+    Act gn = new_act(c, B, x.h, x.w, C);
+    gnorm(c, x, nullptr, a.nw, a.nb, 1e-6f, 0, gn);
+    parts = xf_proj(c, gn.p, M, C, a.piw, fptr(a.pib), h.p, nullptr, B, lnp);
+    drop(c, gn);
+  }
   void* n = c.ws->alloc(M * C * es);
   void* att = c.ws->alloc(M * C * es);
   float2* st = ln_fold_ ? (float2*)c.ws->alloc(M * sizeof(float2)) : nullptr;   // LayerNorm row statistics
@@ -428,7 +485,7 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     g.B = ptr(a.qkvw); g.ldb = C;
     g.C = qkv; g.ldc = 3 * C; g.imgs = B;
     if (hm) { g.hs_L = HW; g.hs_C = C; g.hs_d = d; }
-    ln_gemm(c, g, h.p, M, C, a.ln1w, a.ln1b, a.qkvu, a.qkvv, nullptr, n, st);
+    ln_gemm(c, g, h.p, M, C, a.ln1w, a.ln1b, a.qkvu, a.qkvv, nullptr, n, st, parts);
   }
   if (!c.ws->dry()) {
     AttnArgs aa;
@@ -448,7 +505,7 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     attention(aa, c.s);
   }
   c.ws->free(qkv);
-  linear(c, att, C, M, C, a.o1w, C, fptr(a.o1b), h.p, C, ACT_NONE, h.p, C, 0, B);
+  parts = xf_proj(c, att, M, C, a.o1w, fptr(a.o1b), h.p, h.p, B, lnp);
   // cross-attention (K|V precomputed per prompt)
   {
     GemmArgs g;
@@ -456,7 +513,7 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     g.B = ptr(a.q2w); g.ldb = C;
     g.C = att; g.ldc = C; g.imgs = B;
     if (hm) { g.hs_L = HW; g.hs_C = C; g.hs_d = d; }
-    ln_gemm(c, g, h.p, M, C, a.ln2w, a.ln2b, a.q2u, a.q2v, nullptr, n, st);
+    ln_gemm(c, g, h.p, M, C, a.ln2w, a.ln2b, a.q2u, a.q2v, nullptr, n, st, parts);
   }
   if (!c.ws->dry()) {
     AttnArgs aa;
@@ -469,7 +526,7 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     aa.o = n; aa.ldo = C; aa.so = (long)HW * C;
     attention(aa, c.s);
   }
-  linear(c, n, C, M, C, a.o2w, C, fptr(a.o2b), h.p, C, ACT_NONE, h.p, C, 0, B);
+  parts = xf_proj(c, n, M, C, a.o2w, fptr(a.o2b), h.p, h.p, B, lnp);
   // GEGLU feed-forward: fused into the projection's epilogue when the large-tile path takes the shape
   void* g = c.ws->alloc(M * 4 * C * es);
   {
@@ -480,11 +537,11 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     ga.imgs = B;
     ga.A = h.p; ga.lda = C;
     if (gemm_geglu_fusable(ga)) {
-      ln_gemm(c, ga, h.p, M, C, a.ln3w, a.ln3b, a.ffu, a.ffv, fptr(a.ffb), n, st);
+      ln_gemm(c, ga, h.p, M, C, a.ln3w, a.ln3b, a.ffu, a.ffv, fptr(a.ffb), n, st, parts);
     } else {
       void* ff = c.ws->alloc(M * 8 * C * es);
       ga.geglu = 0; ga.C = ff; ga.ldc = 8 * C;
-      ln_gemm(c, ga, h.p, M, C, a.ln3w, a.ln3b, a.ffu, a.ffv, fptr(a.ffb), n, st);
+      ln_gemm(c, ga, h.p, M, C, a.ln3w, a.ln3b, a.ffu, a.ffv, fptr(a.ffb), n, st, parts);
       if (!c.ws->dry()) geglu(dt_, ff, 8 * C, M, 4 * C, g, 4 * C, 1, c.s);
       c.ws->free(ff);
     }
@@ -494,6 +551,7 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   if (st) c.ws->free(st);
   c.ws->free(att);
   c.ws->free(n);
+  if (lnp) c.ws->free(lnp);
   Act out = new_act(c, B, x.h, x.w, C);
   linear(c, h.p, C, M, C, a.pow, C, fptr(a.pob), out.p, C, ACT_NONE, x.p, C, 0, B, &out);
   drop(c, h);

@@ -153,9 +153,14 @@ class Unet : public Model {
   Act resnet(Ctx& c, const ResW& r, Act& x0, Act* x1, const float* tproj, float eps);
   Act transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L);
   // LayerNorm(x) -> projection g (g.A / lda / bias set here): folded into g's epilogue when ln_fold_ and the shape
-  // takes it (statistics only, written to `st`), else through the normalised copy `nbuf`
+  // takes it — with the statistics from `parts` (the producer of x emitted them, GemmArgs::ln_out) or from a
+  // statistics pass written to `st` — else through the normalised copy `nbuf`
   void ln_gemm(Ctx& c, GemmArgs& g, const void* x, int rows, int C, P lnw, P lnb, P u, P v, const float* bias,
-               void* nbuf, float2* st);
+               void* nbuf, float2* st, const float2* parts = nullptr);
+  // a transformer projection that writes the residual stream (proj_in, to_out, to_out2): out = A W^T + bias
+  // (+ residual), emitting the output's LayerNorm partials into `lnp` where the epilogue can; returns lnp or null
+  const float2* xf_proj(Ctx& c, const void* A, int M, int C, P w, const float* bias, void* out, const void* residual,
+                        int imgs, float2* lnp);
 
   int cin_pad_ = 8;
   bool ln_fold_ = false;   // LayerNorm folded into the transformer projections (fixed at creation: the blob layout)

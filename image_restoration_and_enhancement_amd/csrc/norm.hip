@@ -579,7 +579,55 @@ void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamm
   IRX_LAUNCH_CHECK();
 }
 
+// GroupNorm folded into per-image projection weights (gn_fold_weights): one wave per (output row n, image)
+template <typename T>
+__global__ __launch_bounds__(64) void gn_fold_weights_kernel(const T* __restrict__ W, const float* __restrict__ bias,
+                                                             const float2* __restrict__ ab, int N, int K,
+                                                             T* __restrict__ Wo, float* __restrict__ bo) {
+  const int n = blockIdx.x, img = blockIdx.y, lane = threadIdx.x;
+  const T* w = W + (long)n * K;
+  const float2* a = ab + (long)img * K;
+  T* wo = Wo + ((long)img * N + n) * K;
+  float acc = 0.f;
+  for (int k0 = lane * 8; k0 < K; k0 += 512) {
+    float f[8], o[8];
+    Vec16<T>::unpack(*(const uint4*)(w + k0), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float2 v = a[k0 + e];
+      o[e] = f[e] * v.x;
+      acc = fmaf(f[e], v.y, acc);
+    }
+    *(uint4*)(wo + k0) = Vec16<T>::pack(o);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) bo[(long)img * N + n] = (bias ? bias[n] : 0.f) + acc;
+}
+
 }  // namespace
+
+void group_norm_parts_ab(int C0, int N, int HW, int G, float eps, const float* gamma, const float* beta,
+                         const double* p0, int r0, float2* ab, hipStream_t s) {
+  IRX_CHECK(G > 0 && G <= 64 && C0 % G == 0 && C0 <= kMaxC, "GroupNorm: channel counts");
+  IRX_CHECK(p0 && r0 > 0 && HW % r0 == 0 && ab, "GroupNorm partials missing");
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_finalize_parts_kernel") : std::string(), 0.0, s);
+  gn_finalize_parts_kernel<<<dim3(N, (G + 7) / 8), 256, 0, s>>>((const double2*)p0, C0, HW / r0, nullptr, 0, 0, G,
+                                                                (double)HW * (C0 / G), eps, gamma, beta, ab);
+  IRX_LAUNCH_CHECK();
+}
+
+void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* ab, int N, int K, int imgs, void* Wo,
+                     float* bo, hipStream_t s) {
+  IRX_CHECK(dtype != F32 && K % 8 == 0 && K <= 4096 && N > 0 && imgs > 0, "gn_fold_weights: 16-bit, K % 8 == 0");
+  IRX_CHECK(((uintptr_t)W % 16) == 0 && ((uintptr_t)Wo % 16) == 0, "gn_fold_weights: 16-byte aligned rows");
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_fold_weights_kernel") : std::string(), 0.0, s);
+  if (dtype == F16)
+    gn_fold_weights_kernel<f16_t><<<dim3(N, imgs), 64, 0, s>>>((const f16_t*)W, bias, ab, N, K, (f16_t*)Wo, bo);
+  else
+    gn_fold_weights_kernel<bf16_t><<<dim3(N, imgs), 64, 0, s>>>((const bf16_t*)W, bias, ab, N, K, (bf16_t*)Wo, bo);
+  IRX_LAUNCH_CHECK();
+}
 
 int g_ln_stats8 = 0;   // irx_set_option("ln_stats8", 1): LayerNorm statistics 8 lanes per row (A/B; off until measured on the GPU)
 bool g_gn_v2 = true;   // irx_set_option("gn_v2", 0): v1 LDS-atomic stats + separate finalize (A/B)

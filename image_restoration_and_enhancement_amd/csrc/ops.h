@@ -60,6 +60,18 @@ struct GemmArgs {
   // with ln_rs[m] = (rstd, rstd * mean) of row m of A (layer_norm_stats) and ln_u[n] = sum_k B[n][k]:
   // exactly LN(x) W^T + bias, with no normalised copy of A written or read.
   const float2* ln_rs = nullptr; const float* ln_u = nullptr;
+  // ... or the row statistics as producer partials (ln_out of the GEMM that wrote A): ln_part[m * ln_T + t] = (mean,
+  // M2) of row m over 320-column group t of a ln_T * 320-wide row, merged in the epilogue into
+  // (rstd, rstd * mean) with rstd = rsqrt(M2 / (ln_T * 320) + ln_eps) (ln_rs_at) — no statistics pass over A
+  const float2* ln_part = nullptr; int ln_T = 0; float ln_eps = 1e-5f;
+  // LayerNorm partials of the OUTPUT emitted by the epilogue (gemm_emits_ln_parts: the transformer's residual stream,
+  // whose next consumer folds its LayerNorm): per output row m and 320-column group t, (mean, M2 = sum of squared
+  // deviations from that mean) of the stored values, two-pass over the staged tile, at ln_out[m * (N / 320) + t]
+  float2* ln_out = nullptr;
+  // per-image operands (GroupNorm folded into the weights, gn_fold_weights): rows [i * b_rows, (i + 1) * b_rows) are
+  // multiplied by B + i * b_img_stride and get bias + i * bias_img_stride (0: one B / bias for every row; a tile never
+  // straddles two images: gemm_bimg_ok)
+  int b_rows = 0; long b_img_stride = 0; long bias_img_stride = 0;
   void* splitk_ws = nullptr; size_t splitk_ws_bytes = 0;   // caller workspace for split-K partials
   // (set by the launcher) N-major tile order: consecutive tiles (one XCD's range) share a B panel instead of an A
   // panel — for the weight-heavy small-M shapes (8x8-level convs: 29.5 MB of weights for 1024 rows)
@@ -67,6 +79,32 @@ struct GemmArgs {
   int dbg = 0;            // large-tile diagnostics (irx_set_option("gemm_dbg")): 1 skip epilogue, 2 skip MFMAs
 };
 constexpr int kCanonImages = 16;
+constexpr int kLnGroup = 320;   // columns per LayerNorm partial (GemmArgs::ln_out / ln_part)
+// (rstd, rstd * mean) of row m: ln_rs[m], or merged from the row's ln_T producer partials (equal 320-column groups:
+// mean = the mean of the group means, M2 = sum of the groups' M2 + 320 * sum of squared group-mean deviations)
+__device__ __forceinline__ float2 ln_rs_at(const float2* __restrict__ rs, const float2* __restrict__ part, int T,
+                                           float eps, long m) {
+  if (!part) return rs[m];
+  const float2* p = part + m * T;
+  float mean, m2;
+  if (T == 1) {
+    const float2 v = p[0];
+    mean = v.x;
+    m2 = v.y;
+  } else {
+    float sm = 0.f;
+    for (int t = 0; t < T; ++t) sm += p[t].x;
+    mean = sm / (float)T;
+    m2 = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const float2 v = p[t];
+      const float d = v.x - mean;
+      m2 += fmaf((float)kLnGroup * d, d, v.y);
+    }
+  }
+  const float rstd = rsqrtf(m2 / (float)(T * kLnGroup) + eps);
+  return make_float2(rstd, rstd * mean);
+}
 // element offset of output (m, n) in C (see GemmArgs::hs_L).  Fields passed by value: a reference to the
 // kernel-argument struct would make the compiler copy all of it to scratch.
 __host__ __device__ __forceinline__ long c_off_f(long m, int n, long ldc, int M, int hs_L, int hs_C, int hs_d) {
@@ -86,6 +124,11 @@ size_t gemm_workspace_bytes(const GemmArgs& a);           // split-K partial buf
 bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can apply the GEGLU epilogue
 bool gemm_gn_fusable(const GemmArgs& a);                  // conv can apply GemmArgs::gn_ab to its operand
 bool gemm_ln_foldable(const GemmArgs& a);                 // large-tile epilogue can apply GemmArgs::ln_rs / ln_u
+bool gemm_emits_ln_parts(const GemmArgs& a);              // large-tile epilogue can emit GemmArgs::ln_out
+bool gemm_bimg_ok(const GemmArgs& a);                     // large-tile path can take per-image B / bias (b_rows)
+extern int g_gn_fold;      // 1: the transformer GroupNorm folded into per-image proj_in weights (0: gn_apply, A/B)
+extern int g_geglu_partial; // 1: fused GEGLU also where an image's rows leave partial row tiles (diagnostics)
+extern int g_ln_parts;     // 1: transformer producers emit LayerNorm partials, the statistics pass is skipped (0: A/B)
 extern int g_ln_fold;      // 1: 16-bit UNets fold LayerNorm into the following projections (read at model creation)
 int gemm_emits_gn_parts(const GemmArgs& a);   // rows per GroupNorm partial this call's epilogue emits (0: none)
 extern int g_gn_parts;     // 1: producers emit GroupNorm partial sums, the stats pass is skipped (0: A/B)
@@ -123,6 +166,13 @@ void group_norm_parts(int dtype, const void* x0, const void* x1, int C0, int C1,
 // `ab` [N][C0 + C1] (float2), for a consumer that applies them itself (GemmArgs::gn_ab)
 void group_norm_stats(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
                       const float* gamma, const float* beta, float2* ab, void* ws, hipStream_t s);
+// ... the same scale / shift from producer partials (group_norm_parts' finalize alone; x1 absent)
+void group_norm_parts_ab(int C0, int N, int HW, int G, float eps, const float* gamma, const float* beta,
+                         const double* p0, int r0, float2* ab, hipStream_t s);
+// GroupNorm folded into the projection that consumes it (y = x * a + b per image and channel, then y W^T + bias):
+// Wo[i][n][k] = W[n][k] * ab[i][k].x (rounded to the storage type), bo[i][n] = bias[n] + sum_k W[n][k] * ab[i][k].y
+void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* ab, int N, int K, int imgs, void* Wo,
+                     float* bo, hipStream_t s);
 // gamma / beta may be null: no affine (y = (x - mean) * rstd), the form the folded projections' fallback uses
 void layer_norm(int dtype, const void* x, long ldx, int rows, int C, float eps, const float* gamma,
                 const float* beta, void* out, long ldo, hipStream_t s);

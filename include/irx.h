@@ -269,6 +269,17 @@ int irx_op_geglu(void* stream, int dtype, const void* proj, int M, int F, void* 
 /* C[M][N/2] = GEGLU(A B^T + bias) with B/bias in the GEGLU64 row order (fused epilogue, bf16 large tiles) */
 int irx_op_gemm_geglu(void* stream, int dtype, int M, int N, int K, const void* A, const void* B, const float* bias,
                       void* C);
+/* Transformer residual-stream producer (the diffusers Transformer2D proj_in / attn.to_out at src/inference.py:486's
+   UNet): C = A B^T + bias (+ residual, may alias C), also writing the LayerNorm partials of C's rows:
+   parts[m][N / 320] = (mean, sum of squared deviations) per 320-column group.  Error if the shape cannot emit them. */
+int irx_op_gemm_ln_out(void* stream, int dtype, int M, int N, int K, const void* A, const void* B, const float* bias,
+                       const void* residual, void* C, void* parts);
+/* LayerNorm folded into the following projection (norm1/2/3 -> to_q|k|v / attn2.to_q / ff.net.0.proj):
+   C = rs.x * (A B^T) - rs.y * u + v with B = W diag(gamma), u = row sums of B, v = bias + W beta, and per row
+   rs = (rstd, rstd * mean) of A given directly (rs, from a statistics pass) or merged from T producer partials
+   (parts, irx_op_gemm_ln_out; K = 320 T).  geglu != 0: B / u / v in the GEGLU64 row order, C gets N / 2 columns. */
+int irx_op_gemm_ln_fold(void* stream, int dtype, int M, int N, int K, const void* A, const void* B, const float* u,
+                        const float* v, const void* rs, const void* parts, int T, int geglu, void* C);
 
 #ifdef __cplusplus
 }
