@@ -75,7 +75,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gn_parts", &g_gn_parts, nullptr},
     {"ln_parts", &g_ln_parts, nullptr},
     {"gn_fold", &g_gn_fold, nullptr},
-    {"geglu_partial", &g_geglu_partial, nullptr},
+    {"attn_pipe", &g_attn_pipe, nullptr},
     {"halo_split", &g_halo_split, nullptr},
     {"halo_pipe", &g_halo_pipe, nullptr},
     {"gemm_pp", &g_gemm_pp, nullptr},

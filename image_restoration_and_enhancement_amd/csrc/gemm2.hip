@@ -745,8 +745,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       constexpr int CPR = BN / 8;               // 16-byte chunks per row
       // chunk swizzle inside whole groups of 8 chunks only (BN = 160 leaves a 4-chunk tail unswizzled)
       auto csw = [](int c, int row) { return c < (CPR & ~7) ? c ^ (row & 7) : c; };
-      if (a.ln_rs) {
-        // folded LayerNorm (GemmArgs::ln_rs): y = rstd * acc - rstd * mean * u[n] + bias[n]  (alpha == 1)
+      if (a.ln_rs || a.ln_part) {
+        // folded LayerNorm (GemmArgs::ln_rs / ln_part): y = rstd * acc - rstd * mean * u[n] + bias[n]  (alpha == 1)
         float uu[TN], bb[TN];
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -1271,7 +1271,6 @@ bool gemm_ln_foldable(const GemmArgs& a) {
 }
 
 int g_ln_parts = 1;
-int g_geglu_partial = 0;   // irx_set_option("geglu_partial", 1): fused GEGLU on partial per-image row tiles too (diagnostics)
 
 // The epilogue can emit LayerNorm partials (GemmArgs::ln_out): dense 16-bit large-tile GEMMs whose tiles are 320
 // columns wide (the 64x64 / 32x32-level transformer projections), run by the large-tile kernel's staged epilogue
@@ -1305,14 +1304,10 @@ bool gemm_bimg_ok(const GemmArgs& a) {
 bool gemm_geglu_fusable(const GemmArgs& a) {
   if (!g_large_tiles || !a.geglu || !eligible(a) || !vec_ok(a)) return false;
   if (gemm_sk_eligible(a)) return true;
-  const Choice c = choose(a);
-  if (c.BM == 0) return false;
-  // Fused only where an image's rows fill whole row tiles.  With partial row tiles (the 8x8 level: 64 rows per image,
-  // 256-row tiles, an image count not a multiple of 4) the fused GEGLU epilogue gave fp16 outputs 1-2 ulp apart
-  // between batchings of the same images (test_batch_8_equals_3_plus_5[fp16-256]; bisected to this kernel and shape,
-  // root cause not isolated); the unfused projection + geglu kernel is batch invariant there.
-  if (!g_geglu_partial && a.imgs > 0 && ((long)a.M * a.batch / a.imgs) % c.BM) return false;
-  return true;
+  // (round 3 kept partial per-image row tiles unfused after an fp16 batch dependence; its cause was hipcc fusing the
+  // folded-LayerNorm FMA with the fp16 conversion into v_fma_mixlo_f16 at some unrolled sites only — fixed in
+  // irx_common.h f16_src, tests/test_ln_parts_gpu.py::test_ln_fold_geglu_fp16_batch_invariant)
+  return choose(a).BM != 0;
 }
 
 int halo_bn(const GemmArgs& a);

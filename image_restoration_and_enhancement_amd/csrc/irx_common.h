@@ -33,10 +33,18 @@ template <typename T> __device__ __forceinline__ float ld_f(const T* p);
 template <> __device__ __forceinline__ float ld_f<float>(const float* p) { return *p; }
 template <> __device__ __forceinline__ float ld_f<bf16_t>(const bf16_t* p) { return bf2f(*p); }
 template <> __device__ __forceinline__ float ld_f<f16_t>(const f16_t* p) { return (float)*p; }
+// fp32 -> fp16 always as two steps, the fp32 value first: hipcc otherwise fuses an FMA feeding the conversion into
+// v_fma_mixlo_f16 (one rounding, straight to fp16) at some call sites and not others — the same value then rounds
+// differently with its position in an unrolled epilogue (the round-3 fp16 batch dependence: the folded-LayerNorm
+// GEGLU epilogue, 17330 mixlo instructions in gemm2; scripts/diag_geglu_pos.py).  The empty asm pins the fp32 value.
+__device__ __forceinline__ float f16_src(float f) {
+  asm("" : "+v"(f));
+  return f;
+}
 template <typename T> __device__ __forceinline__ T from_f(float f);
 template <> __device__ __forceinline__ float from_f<float>(float f) { return f; }
 template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float f) { return f2bf(f); }
-template <> __device__ __forceinline__ f16_t from_f<f16_t>(float f) { return (f16_t)f; }   // RNE
+template <> __device__ __forceinline__ f16_t from_f<f16_t>(float f) { return (f16_t)f16_src(f); }   // RNE
 
 // 16-byte vector <-> floats
 template <typename T> struct Vec16;
@@ -80,7 +88,8 @@ template <> struct Vec16<f16_t> {
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      w[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){f[2 * i], f[2 * i + 1]}, f16x2));
+      w[i] = __builtin_bit_cast(uint32_t,
+                                __builtin_convertvector((f32x2){f16_src(f[2 * i]), f16_src(f[2 * i + 1])}, f16x2));
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
@@ -120,9 +129,9 @@ template <> struct Mfma<f16_t> {
                                                  0, 0);
   }
   __device__ static uint32_t pack2(float lo, float hi) {   // one v_cvt_pk_f16_f32 (RNE)
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, f16x2));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){f16_src(lo), f16_src(hi)}, f16x2));
   }
-  __device__ static float round(float x) { return (float)(f16_t)x; }
+  __device__ static float round(float x) { return (float)(f16_t)f16_src(x); }
 };
 
 // ---------------------------------------------------------------- activations (epilogues)

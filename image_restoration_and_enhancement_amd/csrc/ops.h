@@ -127,7 +127,6 @@ bool gemm_ln_foldable(const GemmArgs& a);                 // large-tile epilogue
 bool gemm_emits_ln_parts(const GemmArgs& a);              // large-tile epilogue can emit GemmArgs::ln_out
 bool gemm_bimg_ok(const GemmArgs& a);                     // large-tile path can take per-image B / bias (b_rows)
 extern int g_gn_fold;      // 1: the transformer GroupNorm folded into per-image proj_in weights (0: gn_apply, A/B)
-extern int g_geglu_partial; // 1: fused GEGLU also where an image's rows leave partial row tiles (diagnostics)
 extern int g_ln_parts;     // 1: transformer producers emit LayerNorm partials, the statistics pass is skipped (0: A/B)
 extern int g_ln_fold;      // 1: 16-bit UNets fold LayerNorm into the following projections (read at model creation)
 int gemm_emits_gn_parts(const GemmArgs& a);   // rows per GroupNorm partial this call's epilogue emits (0: none)
@@ -202,6 +201,7 @@ struct AttnArgs {
 void attention(const AttnArgs& a, hipStream_t s);
 extern bool g_attn_v2;
 extern int g_attn_v3;    // 32x32x16 kernel for bf16 / fp16 (0: the round-1 kernels, bf16 only)
+extern int g_attn_pipe;  // 1: non-causal streamed d = 40 attention with QK^T one key tile ahead (attn3p)
 extern int g_attn_prio;
 extern int g_attn_qrep;
 extern int g_attn_xcd;   // 1: (batch, head) groups of q-blocks kept on one XCD (K/V shared in its L2)
