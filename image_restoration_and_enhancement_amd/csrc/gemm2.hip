@@ -249,7 +249,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     }
   };
 
-  if constexpr (HALO == 2) {
+  if constexpr (HALO == 2 || HALO == 3) {
     // ---- ping-pong halo main loop (the default halo path; no GroupNorm-fused operand).  The two waves that
     //      share a SIMD (w and w + 4) take opposite roles in each half of a K step (slab c = kt / 9, tap
     //      t = kt % 9), so one of them always has MFMAs to issue while the other moves data:
@@ -267,6 +267,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     //      and waited for (vmcnt(0): group 0 issues nothing else) at the end of phase 1 of the step before
     //      slab c + 2 starts.
     static_assert(S == 3 && KSUB == 2 && NW == 8, "ping-pong halo: 3-stage B ring, BK 64, 8 waves");
+    // HALO == 3 (option halo_pipe 2): the B panel of a step is split between the groups — group 1 issues its first
+    // BP1 pieces per wave in its load phase (phase 1 of step kt - 2), group 0 the other BPG - BP1 in its own (phase 2
+    // of kt - 2, before that phase's halo pieces) — so neither load phase carries the whole panel's LDS-DMA issue
+    // (the lock-step loop above put all 5 pieces per wave in group 1's phase, 2 halo pieces in 6 of group 0's 9).
+    constexpr bool BAL = HALO == 3;
     const int W = a.g.Win, H = a.g.Hin, lw = __builtin_ctz(W);
     const int HW = H * W;
     const int img = m0 / HW, y0 = (m0 - img * HW) >> lw;
@@ -277,6 +282,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     static_assert(HPG * RPI * NG == BM + 2 * kHaloWMax && HPP * HPARTS == HPG, "halo pieces");
     constexpr int NBI = BN / RPI, BPG = NBI / NG;          // B wave-instructions per step, per group-1 wave
     static_assert(BPG * NG == NBI, "B pieces");
+    constexpr int BP1 = BAL ? (BPG + 1) / 2 : BPG, BP0 = BPG - BP1;   // per wave: group 1's / group 0's pieces
     const int wv = __builtin_amdgcn_readfirstlane(wave);   // (scalar: the role branches stay uniform)
     const bool g1 = wv >= NG;
     const int gw = wv - (g1 ? NG : 0);
@@ -292,17 +298,22 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       const int q = gw * BPG + j, r = RPI * q + lane / CPR;
       bro[j] = n0 + r < a.N ? Bp + (long)(n0 + r) * a.ldb + (((lane % CPR) ^ swz(r)) * 8) : nullptr;
     }
-    auto issueB = [&](int kt) {   // group 1: all of B(kt)
+    // pieces [j0, j1) of this wave's BPG-piece share of B(kt) (group 1: [0, BP1), group 0: [BP1, BPG))
+    auto issueB = [&](int kt, auto j0c, auto j1c) {
+      constexpr int j0 = decltype(j0c)::value, j1 = decltype(j1c)::value;
       if (a.dbg & 4) return;      // (timing diagnostics: no B DMA)
       const int c = kt / 9, t = kt - 9 * c;
       const int off = t * Cin + c * BK;
       uint4* const st = Bsm + (kt % S) * BN * CPR;
 #pragma unroll
-      for (int j = 0; j < BPG; ++j) {
+      for (int j = j0; j < j1; ++j) {
         uint4* dst = st + (gw * BPG + j) * 64;
         glds16_asm(bro[j] ? bro[j] + off : zp, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
       }
     };
+    using I0 = std::integral_constant<int, 0>;
+    using IP1 = std::integral_constant<int, BP1>;
+    using IPG = std::integral_constant<int, BPG>;
     auto issueH = [&](int c, int j0, int j1) {   // group 0: pieces [j0, j1) of slab c's halo
       if (a.dbg & 8) return;      // (timing diagnostics: no halo DMA)
       const bool second = c * BK >= a.g.C0;
@@ -377,13 +388,16 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     // this split's K steps [kt0, nk): whole slabs (host: sp.per is a multiple of 9); >= 9 steps per split
     const int nk = kt1, c0 = kt0 / 9, cend = (kt1 + 8) / 9;
     if (g1) {
-      issueB(kt0);
-      issueB(kt0 + 1);
-      wait_vm(BPG);                                      // B(kt0) landed
+      issueB(kt0, I0{}, IP1{});
+      issueB(kt0 + 1, I0{}, IP1{});
+      wait_vm(BP1);                                      // B(kt0) landed
     } else {
+      if constexpr (BAL) issueB(kt0, IP1{}, IPG{});
       issueH(c0, 0, HPG);
+      if constexpr (BAL) issueB(kt0 + 1, IP1{}, IPG{});
       if (c0 + 1 < cend) issueH(c0 + 1, 0, HPG);
-      wait_vm(c0 + 1 < cend ? HPG : 0);                   // H(c0) landed
+      // B(kt0) and H(c0) landed (group 0's part of B(kt0 + 1) is waited for in its first compute phase)
+      wait_vm((BAL ? BP0 : 0) + (c0 + 1 < cend ? HPG : 0));
     }
     barrier();                                           // (+ the zero row)
     // one program for both groups: every wave runs {load phase of step k; barrier; compute phase of step k;
@@ -399,19 +413,31 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         const int kt = 9 * c + t;
         // ---- load phase
         if (g1) {
-          if (!(last && t >= 7)) issueB(kt + 2);
-        } else if (t < HPARTS && halo_next) {
-          issueH(c + 1, t * HPP, (t + 1) * HPP);
+          if (!(last && t >= 7)) issueB(kt + 2, I0{}, IP1{});
+        } else {
+          if constexpr (BAL) {
+            if (!(last && t >= 7)) issueB(kt + 2, IP1{}, IPG{});
+          }
+          if (t < HPARTS && halo_next) issueH(c + 1, t * HPP, (t + 1) * HPP);
         }
         readF(tc, Hs);
         if (g1 && !(last && t == 8)) {                   // B(kt + 1) landed (group 0 reads it next)
           if (last && t == 7) wait_vm(0);
-          else wait_vm(BPG);
+          else wait_vm(BP1);
         }
         barrier();
         // ---- compute phase
         mma();
-        if (!g1 && t == 8 && !last) wait_vm(0);          // the next slab's halo landed
+        if (!g1) {
+          if (t == 8 && !last) {
+            wait_vm(0);                                  // the next slab's halo landed (and B(kt + 1))
+          } else if constexpr (BAL) {
+            // group 0's part of B(kt + 1), issued in its previous load phase before that phase's halo pieces
+            const int hprev = t == 0 ? (c == c0 && c0 + 1 < cend ? HPG : 0)
+                                     : ((t - 1) < HPARTS && halo_next ? HPP : 0);
+            wait_vm(hprev);
+          }
+        }
         barrier();
         (void)kt;
       });
@@ -754,13 +780,23 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           uu[j] = n < a.N ? a.ln_u[n] : 0.f;
           bb[j] = (biasp && n < a.N) ? biasp[n] : 0.f;
         }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
+        // the four rows of accumulator block i + 1 are fetched (and merged) while block i is stored
+        float2 rsc[4], rsn[4];
+        auto fetch_rs = [&](int i, float2* dst) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = wm * TM * 16 + i * 16 + fgrp * 4 + r;
-            const float2 rs = m0 + row < a.M ? ln_rs_at(a.ln_rs, a.ln_part, a.ln_T, a.ln_eps, m0 + row)
-                                             : make_float2(0.f, 0.f);
+            dst[r] = m0 + row < a.M ? ln_rs_at(a.ln_rs, a.ln_part, a.ln_T, a.ln_eps, m0 + row) : make_float2(0.f, 0.f);
+          }
+        };
+        fetch_rs(0, rsc);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          if (i + 1 < TM) fetch_rs(i + 1, rsn);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = wm * TM * 16 + i * 16 + fgrp * 4 + r;
+            const float2 rs = rsc[r];
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
               const int col = wn * TN * 16 + j * 16 + frow;
@@ -768,6 +804,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
                   __builtin_bit_cast(uint16_t, from_f<T>(fmaf(acc[i][j][r], rs.x, fmaf(-rs.y, uu[j], bb[j]))));
             }
           }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rsc[r] = rsn[r];
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -949,33 +988,36 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           constexpr int G = NT / BM, CPG = CPR / G;
           static_assert(CPR % G == 0 && (G == 1 || G == 2 || G == 4 || G == 8), "LayerNorm partial lanes");
           __syncthreads();
+          // one pass of sums shifted by the row's first stored value x0: d = x - x0, mean = x0 + sum d / n,
+          // M2 = sum d^2 - (sum d)^2 / n (x0 is a sample of the row, so the subtraction loses little)
           const int row = tid / G, g = tid % G;
           const uint16_t* trow = tileS + row * BN;
-          float s1 = 0.f;
-#pragma unroll 4
-          for (int c = g * CPG; c < (g + 1) * CPG; ++c) {
-            float f[8];
-            Vec16<T>::unpack(*(const uint4*)(trow + (csw(c, row) << 3)), f);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) s1 += f[e];
+          float x0;
+          {
+            float f0[8];
+            Vec16<T>::unpack(*(const uint4*)(trow + (csw(0, row) << 3)), f0);
+            x0 = f0[0];
           }
-#pragma unroll
-          for (int o = 1; o < G; o <<= 1) s1 += __shfl_xor(s1, o);
-          const float mean = s1 / (float)kLnGroup;
-          float s2 = 0.f;
+          float s1 = 0.f, s2 = 0.f;
 #pragma unroll 4
           for (int c = g * CPG; c < (g + 1) * CPG; ++c) {
             float f[8];
             Vec16<T>::unpack(*(const uint4*)(trow + (csw(c, row) << 3)), f);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float d = f[e] - mean;
+              const float d = f[e] - x0;
+              s1 += d;
               s2 = fmaf(d, d, s2);
             }
           }
 #pragma unroll
-          for (int o = 1; o < G; o <<= 1) s2 += __shfl_xor(s2, o);
-          if (g == 0 && m0 + row < a.M) lno[(long)(m0 + row) * (a.N / kLnGroup) + n0 / kLnGroup] = make_float2(mean, s2);
+          for (int o = 1; o < G; o <<= 1) {
+            s1 += __shfl_xor(s1, o);
+            s2 += __shfl_xor(s2, o);
+          }
+          const float ds = s1 * (1.f / (float)kLnGroup);
+          if (g == 0 && m0 + row < a.M)
+            lno[(long)(m0 + row) * (a.N / kLnGroup) + n0 / kLnGroup] = make_float2(x0 + ds, fmaxf(fmaf(-s1, ds, s2), 0.f));
         }
       }
       return;
@@ -1388,7 +1430,8 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
       sp.inkernel = true;
       sp.cnt = stream_counters(s);
     }
-    if (g_halo_pipe && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 2>(b, sp, s);   // software-pipelined main loop
+    if (g_halo_pipe == 2 && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 3>(b, sp, s);   // ping-pong, B split by group
+    else if (g_halo_pipe && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 2>(b, sp, s);   // ping-pong main loop
     else launch2<256, 160, 4, 2, 64, 3, 1>(b, sp, s);
     return true;
   }

@@ -312,10 +312,7 @@ __global__ __launch_bounds__(256, BPC) void gemm_sk_kernel(GemmArgs a, int n_sli
       for (int ih = 0; ih < 2; ++ih) {
         const int i = 2 * rr + ih;
         float2 rs = has_ln ? lst[i * 16 + (lane & 15)] : make_float2(1.f, 0.f);
-        if (a.ln_part) {   // producer partial (mean, M2) -> (rstd, rstd * mean): ln_rs_at's arithmetic for one group
-          const float rstd = rsqrtf(rs.y / (float)kLnGroup + a.ln_eps);
-          rs = make_float2(rstd, rstd * rs.x);
-        }
+        if (a.ln_part) rs = ln_fin(rs.x, rs.y, 1, a.ln_eps);   // producer partial (mean, M2): ln_rs_at's arithmetic
         float v[NB][4];
 #pragma unroll
         for (int j = 0; j < NB; ++j) {

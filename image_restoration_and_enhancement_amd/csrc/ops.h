@@ -80,30 +80,39 @@ struct GemmArgs {
 };
 constexpr int kCanonImages = 16;
 constexpr int kLnGroup = 320;   // columns per LayerNorm partial (GemmArgs::ln_out / ln_part)
-// (rstd, rstd * mean) of row m: ln_rs[m], or merged from the row's ln_T producer partials (equal 320-column groups:
-// mean = the mean of the group means, M2 = sum of the groups' M2 + 320 * sum of squared group-mean deviations)
+// LayerNorm row statistics from producer partials (mean_t, M2_t) over T equal 320-column groups: the merged (mean, M2)
+// (two groups: M2 = M2_a + M2_b + 160 (mean_a - mean_b)^2; mean = (mean_a + mean_b) / 2, both exact reassociations of
+// the pooled sums) and the (rstd, rstd * mean) the folded epilogue applies.  Multiplies by exact reciprocals only
+// (no division): the same arithmetic wherever it runs (gemm2 / gemm_sk epilogues).
+__device__ __forceinline__ float2 ln_fin(float mean, float m2, int T, float eps) {
+  const float inv_n = T == 1 ? 1.f / 320.f : T == 2 ? 1.f / 640.f : 1.f / (float)(T * kLnGroup);
+  const float rstd = rsqrtf(fmaf(m2, inv_n, eps));
+  return make_float2(rstd, rstd * mean);
+}
+__device__ __forceinline__ float2 ln_merge(const float2* __restrict__ p, int T) {   // -> (mean, M2)
+  if (T == 1) return p[0];
+  if (T == 2) {
+    const float2 x = p[0], y = p[1];
+    const float d = x.x - y.x;
+    return make_float2((x.x + y.x) * 0.5f, fmaf(0.5f * (float)kLnGroup * d, d, x.y + y.y));
+  }
+  float sm = 0.f;
+  for (int t = 0; t < T; ++t) sm += p[t].x;
+  const float mean = sm * (1.f / (float)T);
+  float m2 = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float2 v = p[t];
+    const float d = v.x - mean;
+    m2 += fmaf((float)kLnGroup * d, d, v.y);
+  }
+  return make_float2(mean, m2);
+}
+// (rstd, rstd * mean) of row m: ln_rs[m], or merged from the row's ln_T producer partials
 __device__ __forceinline__ float2 ln_rs_at(const float2* __restrict__ rs, const float2* __restrict__ part, int T,
                                            float eps, long m) {
   if (!part) return rs[m];
-  const float2* p = part + m * T;
-  float mean, m2;
-  if (T == 1) {
-    const float2 v = p[0];
-    mean = v.x;
-    m2 = v.y;
-  } else {
-    float sm = 0.f;
-    for (int t = 0; t < T; ++t) sm += p[t].x;
-    mean = sm / (float)T;
-    m2 = 0.f;
-    for (int t = 0; t < T; ++t) {
-      const float2 v = p[t];
-      const float d = v.x - mean;
-      m2 += fmaf((float)kLnGroup * d, d, v.y);
-    }
-  }
-  const float rstd = rsqrtf(m2 / (float)(T * kLnGroup) + eps);
-  return make_float2(rstd, rstd * mean);
+  const float2 v = ln_merge(part + m * T, T);
+  return ln_fin(v.x, v.y, T, eps);
 }
 // element offset of output (m, n) in C (see GemmArgs::hs_L).  Fields passed by value: a reference to the
 // kernel-argument struct would make the compiler copy all of it to scratch.

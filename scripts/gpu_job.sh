@@ -18,6 +18,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
+export IRX_PROF_TOP=${IRX_PROF_TOP:-60}   # bench.py: kernels listed in the profiled step's log
 tag=$1; shift
 O=gpurun_out/$tag
 mkdir -p "$O"

@@ -8,7 +8,8 @@ projection (ln_fold); with ln_parts the projection that writes h also emits, per
 
 Checked here through the C ABI (irx_op_gemm_ln_out / irx_op_gemm_ln_fold):
   * the producer's outputs are bit-identical with and without the emission, and its partials equal the fp64
-    two-pass statistics of the stored rows (|d mean| <= 1e-5 of the row's max |x|, M2 relative 1e-5);
+    two-pass statistics of the stored rows (|d mean| <= 1e-5 of the row's max |x|, M2 relative 5e-5: the epilogue
+    makes one fp32 pass of sums shifted by the row's first value);
   * the folded consumer fed the partials matches PyTorch fp32 LayerNorm + projection within the dtype bound, and
     the consumer fed the same statistics as (rstd, rstd * mean) rows within one ulp of its output;
   * GEGLU consumers (K = 320 streaming kernel, K = 640 large tiles with two partials per row);
@@ -72,7 +73,7 @@ def test_ln_out_partials(device, dt, M, C, res):
     scale = out.float().abs().amax(-1, keepdim=True).double()
     assert torch.isfinite(parts).all()
     assert float(((parts[..., 0].double() - mean).abs() / scale).max()) < 1e-5
-    assert float(((parts[..., 1].double() - m2).abs() / m2).max()) < 1e-5
+    assert float(((parts[..., 1].double() - m2).abs() / m2).max()) < 5e-5     # (one shifted fp32 pass)
 
 
 def _ln_fold_operands(C, N, seed, geglu):
@@ -113,10 +114,11 @@ def test_ln_fold_from_partials(device, dt, M, C, N, geglu):
     got = fold_gemm(h, Wg, u, v, dt, device, parts=parts, T=C // 320, geglu=geglu)
     # the same statistics handed over as rows (rstd, rstd * mean), computed in fp32 from the partials the way
     # the epilogue merges them
-    pm, pq = parts[..., 0], parts[..., 1]
+    pm, pq = parts[..., 0].double(), parts[..., 1].double()
     mean = pm.mean(-1)
     m2 = (pq + 320.0 * (pm - mean[:, None]) ** 2).sum(-1)
     rstd = torch.rsqrt(m2 / C + 1e-5)
+    mean, rstd = mean.float(), rstd.float()
     rs = torch.stack([rstd, rstd * mean], -1).contiguous()
     via_rs = fold_gemm(h, Wg, u, v, dt, device, rs=rs, geglu=geglu)
     torch.cuda.synchronize()
