@@ -130,7 +130,7 @@ _SIGS = {
     "irx_op_attention_hm": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32]),
     "irx_op_geglu": (i32, [vp, i32, vp, i32, i32, vp]),
     "irx_op_gemm_geglu": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, vp]),
-    "irx_op_gemm_ln_out": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+    "irx_op_gemm_ln_out": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, f32]),
     "irx_op_gemm_ln_fold": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, i32, vp]),
 }
 

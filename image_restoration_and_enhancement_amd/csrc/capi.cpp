@@ -76,6 +76,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"ln_parts", &g_ln_parts, nullptr},
     {"gn_fold", &g_gn_fold, nullptr},
     {"attn_pipe", &g_attn_pipe, nullptr},
+    {"halo_prio", &g_halo_prio, nullptr},
     {"halo_split", &g_halo_split, nullptr},
     {"halo_pipe", &g_halo_pipe, nullptr},
     {"gemm_pp", &g_gemm_pp, nullptr},
@@ -657,7 +658,7 @@ int irx_op_attention_hm(void* s, int dtype, int B, int H, int lq, int lk, int d,
 }
 
 int irx_op_gemm_ln_out(void* s, int dtype, int M, int N, int K, const void* A, const void* B, const float* bias,
-                       const void* residual, void* C, void* parts) {
+                       const void* residual, void* C, void* parts, int final_rs, float eps) {
   IRX_API_BEGIN
   GemmArgs a;
   a.dtype = dtype; a.M = M; a.N = N; a.K = K;
@@ -665,6 +666,8 @@ int irx_op_gemm_ln_out(void* s, int dtype, int M, int N, int K, const void* A, c
   a.C = C; a.ldc = N; a.bias = bias;
   a.residual = residual; a.ldr = N;
   a.imgs = g_op_imgs;
+  a.ln_out_rs = final_rs;
+  a.ln_eps = eps;
   IRX_CHECK(parts && gemm_emits_ln_parts(a), "shape/dtype cannot emit LayerNorm partials");
   a.ln_out = (float2*)parts;
   gemm(a, S(s));

@@ -371,14 +371,20 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         for (int j = 0; j < TN; ++j) fb[ss][j] = Bs[boff[ss] + j * 16 * CPR];
       }
     };
+    const bool pmma = (a.prio & 1) != 0;
     auto mma = [&]() {
       if (a.dbg & 2) return;
+      if (pmma) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
       for (int ss = 0; ss < KSUB; ++ss)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[ss][i], fb[ss][j], acc[i][j]);
+      if (pmma) {
+        if ((a.prio & 2) && g1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
     };
     const bool nobar = (a.dbg & 32) != 0;   // (timing diagnostics: no barriers)
     auto barrier = [&] {
@@ -400,6 +406,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       wait_vm((BAL ? BP0 : 0) + (c0 + 1 < cend ? HPG : 0));
     }
     barrier();                                           // (+ the zero row)
+    if ((a.prio & 2) && g1) __builtin_amdgcn_s_setprio(1);   // (static priority for the second-dispatched half)
     // one program for both groups: every wave runs {load phase of step k; barrier; compute phase of step k;
     // barrier}, group 1 one phase behind group 0 (one extra barrier in front, group 0 one extra at the end),
     // so each interval between barriers pairs one group's MFMAs with the other group's loads
@@ -443,6 +450,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       });
     }
     if (!g1) barrier();
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   } else if constexpr (HALO == 1) {
@@ -769,6 +777,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       uint16_t* tileS = (uint16_t*)smem;
       uint16_t* Cp = (uint16_t*)a.C + (long)z * a.sC;
       constexpr int CPR = BN / 8;               // 16-byte chunks per row
+      // residual / row-add operands of the store passes requested before the first store (not for the 128x128 tiles:
+      // two of them stay resident per CU only within 128 VGPRs)
+      constexpr bool kEpiPrefetch = !(BM == 128 && BN == 128) && NW == 8;
       // chunk swizzle inside whole groups of 8 chunks only (BN = 160 leaves a 4-chunk tail unswizzled)
       auto csw = [](int c, int row) { return c < (CPR & ~7) ? c ^ (row & 7) : c; };
       if (a.ln_rs || a.ln_part) {
@@ -908,13 +919,55 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         };
         if (colok) {
           const int rend = min(BM, a.M - m0);
-          // (one row per step: a two-row software pipeline here pushed the 128x128 tiles past 128 VGPRs,
-          //  i.e. from two resident blocks per CU to one)
+          if constexpr (kEpiPrefetch) {
+            // every residual chunk of this thread's rows is requested before the first store (one memory latency
+            // per tile instead of one per row: the stores may alias the residual, so the compiler cannot hoist the
+            // loads itself); the row add is one vector per image, loaded once when the tile lies in one image
+            constexpr int KMAX = (BM + RS - 1) / RS;
+            uint4 rres[KMAX];
+            if (Rp) {
+#pragma unroll
+              for (int k = 0; k < KMAX; ++k) {
+                const int row = min(rg + k * RS, rend - 1);   // (clamped, not branched: one batch of loads)
+                rres[k] = *(const uint4*)(Rp + (long)(m0 + row) * a.ldr + n0 + cc * 8);
+              }
+            }
+            const bool ra1 = a.rowadd && (m0 / a.rows_per_group) == ((m0 + rend - 1) / a.rows_per_group);
+            float4 rx = make_float4(0.f, 0.f, 0.f, 0.f), ry = rx;
+            if (ra1) {
+              const float4* ra = (const float4*)(a.rowadd + (long)(m0 / a.rows_per_group) * a.rowadd_ld + n0 + cc * 8);
+              rx = ra[0];
+              ry = ra[1];
+            }
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k) {
+              const int row = rg + k * RS;
+              if (row >= rend) break;
+              Src q;
+              q.u = *(const uint4*)(tileS + row * BN + (csw(cc, row) << 3));
+              q.r = rres[k];
+              if (a.rowadd) {
+                if (ra1) {
+                  q.x = rx;
+                  q.y = ry;
+                } else {
+                  const float4* ra = (const float4*)(a.rowadd + (long)((m0 + row) / a.rows_per_group) * a.rowadd_ld +
+                                                     n0 + cc * 8);
+                  q.x = ra[0];
+                  q.y = ra[1];
+                }
+              }
+              acc(combine(row, cc, q));
+            }
+          } else {
+            // (one row per step: a two-row software pipeline here pushed the 128x128 tiles past 128 VGPRs,
+            //  i.e. from two resident blocks per CU to one)
 #pragma unroll 1
-          for (int row = rg; row < rend; row += RS) {
-            Src q0;
-            fetch(row, cc, q0);
-            acc(combine(row, cc, q0));
+            for (int row = rg; row < rend; row += RS) {
+              Src q0;
+              fetch(row, cc, q0);
+              acc(combine(row, cc, q0));
+            }
           }
         }
         __syncthreads();        // every read of the staged tile is done before `red` overlays it
@@ -954,8 +1007,24 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       // LayerNorm partials of the output (GemmArgs::ln_out; host: gemm_emits_ln_parts, BN == kLnGroup): the final
       // values are written back over the staged tile, then G threads per row reduce it in two passes
       float2* const lno = BN == kLnGroup ? a.ln_out : nullptr;
+      // residual chunks of all this thread's iterations requested up front (as in the GroupNorm-partial loop above)
+      constexpr int KIT = kEpiPrefetch ? (BM * CPR + NT - 1) / NT : 1;
+      uint4 rres[KIT];
+      if constexpr (kEpiPrefetch) {
+        if (Rp) {
+#pragma unroll
+          for (int k = 0; k < KIT; ++k) {
+            const int idx = min(tid + k * NT, BM * CPR - 1);
+            const int row = idx / CPR, c = idx - row * CPR;
+            const int m = min(m0 + row, a.M - 1), n = min(n0 + c * 8, a.N - 8);
+            rres[k] = *(const uint4*)(Rp + (long)m * a.ldr + n);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < KIT; ++k) {
 #pragma unroll 1
-      for (int idx = tid; idx < BM * CPR; idx += NT) {
+      for (int idx = tid + k * NT; idx < BM * CPR; idx += (kEpiPrefetch ? BM * CPR : NT)) {
         const int row = idx / CPR, c = idx - row * CPR;
         const int m = m0 + row, n = n0 + c * 8;
         if (m >= a.M || n >= a.N) continue;
@@ -971,7 +1040,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           }
           if (Rp) {
             float rv[8];
-            Vec16<T>::unpack(*(const uint4*)(Rp + (long)m * a.ldr + n), rv);
+            Vec16<T>::unpack(kEpiPrefetch ? rres[k] : *(const uint4*)(Rp + (long)m * a.ldr + n), rv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] += rv[e];
           }
@@ -981,6 +1050,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           if (lno) *ts = u;
         }
         *(uint4*)(Cp + c_off(a, m, n)) = u;
+      }
       }
       if constexpr (BN == kLnGroup && NT % BM == 0) {
         if (lno) {
@@ -1016,8 +1086,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
             s2 += __shfl_xor(s2, o);
           }
           const float ds = s1 * (1.f / (float)kLnGroup);
-          if (g == 0 && m0 + row < a.M)
-            lno[(long)(m0 + row) * (a.N / kLnGroup) + n0 / kLnGroup] = make_float2(x0 + ds, fmaxf(fmaf(-s1, ds, s2), 0.f));
+          if (g == 0 && m0 + row < a.M) {
+            const float mean = x0 + ds, m2 = fmaxf(fmaf(-s1, ds, s2), 0.f);
+            lno[(long)(m0 + row) * (a.N / kLnGroup) + n0 / kLnGroup] =
+                a.ln_out_rs ? ln_fin(mean, m2, 1, a.ln_eps) : make_float2(mean, m2);
+          }
         }
       }
       return;
@@ -1319,6 +1392,7 @@ int g_ln_parts = 1;
 bool gemm_emits_ln_parts(const GemmArgs& a) {
   if (!g_ln_parts || !g_large_tiles || !is16(a.dtype) || a.conv || a.geglu || a.hs_L || a.batch != 1 || a.out_f32) return false;
   if (a.gn_part || a.N % kLnGroup != 0 || !eligible(a) || !vec_ok(a) || gemm_sk_eligible(a)) return false;
+  if (a.ln_out_rs && a.N != kLnGroup) return false;
   const Choice c = choose(a);
   if (c.BN != kLnGroup || c.small || (c.BM != 256 && c.BM != 128)) return false;
   if (c.splits > 1) {   // only the in-kernel reduction runs the full epilogue
@@ -1372,6 +1446,7 @@ size_t gemm_workspace_bytes(const GemmArgs& a) {
 // reduction) when two splits do, 0 = the halo path does not take the shape.
 int g_halo_split = 1;   // irx_set_option("halo_split", 0): no K-split halo tiles (A/B)
 int g_halo_pipe = 1;    // irx_set_option("halo_pipe", 0): the round-2 halo main loop (A/B)
+int g_halo_prio = 0;    // irx_set_option("halo_prio", m): ping-pong halo wave priorities (GemmArgs::prio; A/B)
 // irx_set_option("gemm_pp", 1): ping-pong main loop for dense GEMMs / im2col convs.  Off: measured slower at every
 // UNet / VAE shape (bench 553.8 vs 515.7 ms/step, the VAE 512x512 convs 1.9x; profiles/r03_kbench_*_pp.txt) — the
 // halo conv's gain came with its unrolled-tap addressing, which these loops do not need
@@ -1416,6 +1491,7 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     GemmArgs b = a;
     b.vec_epilogue = 1;
     b.dbg = g_gemm_dbg;
+    b.prio = g_halo_prio;
     Split sp;
     sp.per = a.K / 64;
     const int splits = halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));

@@ -390,13 +390,7 @@ void Unet::ln_gemm(Ctx& c, GemmArgs& g, const void* x, int rows, int C, P lnw, P
     g.bias = fptr(v);                 // bias + W beta
     g.A = x;
     g.ln_u = fptr(u);
-    if (parts) {                      // statistics from the producer's partials: no pass over x
-      g.ln_part = parts;
-      g.ln_T = C / kLnGroup;
-      g.ln_eps = 1e-5f;
-    } else {
-      g.ln_rs = st;
-    }
+    g.ln_rs = parts ? parts : st;     // (the producer of x wrote its rows' statistics: no pass over x)
     if (gemm_ln_foldable(g)) {
       if (!parts && !c.ws->dry()) layer_norm_stats(dt_, x, C, rows, C, 1e-5f, st, c.s);
     } else {                          // (W * gamma, bias + W beta) after an affine-free LayerNorm
@@ -421,6 +415,8 @@ const float2* Unet::xf_proj(Ctx& c, const void* A, int M, int C, P w, const floa
   a.bias = bias;
   a.residual = residual; a.ldr = C;
   a.imgs = imgs;
+  a.ln_out_rs = 1;
+  a.ln_eps = 1e-5f;
   const bool emit = lnp && gemm_emits_ln_parts(a);   // (shape-only decision: the dry run decides the same)
   if (emit) a.ln_out = lnp;
   run_gemm(c, a);
@@ -434,11 +430,14 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   const int heads = cfg_.heads, d = C / heads;
   const float scale = 1.0f / std::sqrt((float)d);
   Act h = new_act(c, B, x.h, x.w, C);
-  // LayerNorm partials of the residual stream h, emitted by the projections that write it (GemmArgs::ln_out)
-  float2* lnp = (ln_fold_ && C % kLnGroup == 0) ? (float2*)c.ws->alloc(M * (C / kLnGroup) * sizeof(float2)) : nullptr;
+  // LayerNorm row statistics of the residual stream h, written by the projections that write it (GemmArgs::ln_out,
+  // final (rstd, rstd * mean) rows: C == 320, the 64x64 level, where a 320-column tile holds the whole row; the
+  // wider levels keep the statistics pass — their two-partial merge in the consumers' epilogues measured slower)
+  float2* lnp = (ln_fold_ && C == kLnGroup) ? (float2*)c.ws->alloc(M * sizeof(float2)) : nullptr;
   const float2* parts = nullptr;
   // GroupNorm (no SiLU) -> proj_in: folded into per-image weights where they stay small next to the activation
-  // (C <= 640, i.e. the 64x64 / 32x32 levels): proj_in(GN(x)) = x (W diag(a_i))^T + (bias + W b_i) for image i with
+  // (C == 320, the 64x64 level: 16 x 200 KB against 2 x 42 MB of gn_apply traffic; at 32x32 the 13 MB of per-image
+  // weights cost what they save): proj_in(GN(x)) = x (W diag(a_i))^T + (bias + W b_i) for image i with
   // GN(x) = x * a_i + b_i per channel — the normalised tensor is neither written nor read
   GemmArgs pg;
   pg.dtype = dt_; pg.M = M; pg.N = C; pg.K = C;
@@ -447,7 +446,7 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
   pg.imgs = B;
   pg.b_rows = HW; pg.b_img_stride = (long)C * C; pg.bias_img_stride = C;
   pg.B = ptr(a.piw);   // (placeholder for the shape checks: the folded copies replace it below)
-  if (dt_ != F32 && g_gn_fold && C <= 640 && x.gnp && HW % x.gnr == 0 && gemm_bimg_ok(pg)) {
+  if (dt_ != F32 && g_gn_fold && C <= 320 && x.gnp && HW % x.gnr == 0 && gemm_bimg_ok(pg)) {
     float2* ab = (float2*)c.ws->alloc((size_t)B * C * sizeof(float2));
     void* wf = c.ws->alloc((size_t)B * C * C * es);
     float* bf = (float*)c.ws->alloc((size_t)B * C * sizeof(float));
@@ -457,6 +456,8 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     }
     pg.B = wf;
     pg.bias = bf;
+    pg.ln_out_rs = 1;
+    pg.ln_eps = 1e-5f;
     if (lnp && gemm_emits_ln_parts(pg)) {
       pg.ln_out = lnp;
       parts = lnp;

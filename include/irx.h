@@ -270,10 +270,12 @@ int irx_op_geglu(void* stream, int dtype, const void* proj, int M, int F, void* 
 int irx_op_gemm_geglu(void* stream, int dtype, int M, int N, int K, const void* A, const void* B, const float* bias,
                       void* C);
 /* Transformer residual-stream producer (the diffusers Transformer2D proj_in / attn.to_out at src/inference.py:486's
-   UNet): C = A B^T + bias (+ residual, may alias C), also writing the LayerNorm partials of C's rows:
-   parts[m][N / 320] = (mean, sum of squared deviations) per 320-column group.  Error if the shape cannot emit them. */
+   UNet): C = A B^T + bias (+ residual, may alias C), also writing the LayerNorm statistics of C's rows:
+   final_rs == 0: parts[m][N / 320] = (mean, sum of squared deviations) per 320-column group;
+   final_rs != 0 (N == 320): parts[m] = (rstd, rstd * mean) with rstd = rsqrt(var + eps), the folded consumer's rs.
+   Error if the shape cannot emit them. */
 int irx_op_gemm_ln_out(void* stream, int dtype, int M, int N, int K, const void* A, const void* B, const float* bias,
-                       const void* residual, void* C, void* parts);
+                       const void* residual, void* C, void* parts, int final_rs, float eps);
 /* LayerNorm folded into the following projection (norm1/2/3 -> to_q|k|v / attn2.to_q / ff.net.0.proj):
    C = rs.x * (A B^T) - rs.y * u + v with B = W diag(gamma), u = row sums of B, v = bias + W beta, and per row
    rs = (rstd, rstd * mean) of A given directly (rs, from a statistics pass) or merged from T producer partials

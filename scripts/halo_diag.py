@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--dbg", default="0,1,2,4,8,12,16,32,20,36")
     ap.add_argument("--opt", action="append", default=[])
+    ap.add_argument("--variants", default="",
+                    help="option sets to A/B instead of the dbg bits, interleaved: 'name:k=v,k=v;name2:k=v'")
     a = ap.parse_args()
     L.load()
     for o in a.opt:
@@ -39,7 +41,13 @@ def main():
         L.call("irx_set_option", k.encode(), int(v))
     dev, dt = torch.device("cuda"), torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
-    dbgs = [int(x) for x in a.dbg.split(",")]
+    if a.variants:   # (name, {option: value}) sets, timed at dbg 0
+        sets = []
+        for part in a.variants.split(";"):
+            name, _, kv = part.partition(":")
+            sets.append((name, {k: int(v) for k, v in (x.split("=") for x in kv.split(",") if x)}))
+    else:
+        sets = [(f"dbg {int(x):3d}", {"gemm_dbg": int(x)}) for x in a.dbg.split(",")]
     for lab, N, H, W, C0, C1, Co in SHAPES:
         x0 = torch.randn(N, H, W, C0, device=dev, generator=g).to(dt)
         x1 = torch.randn(N, H, W, C1, device=dev, generator=g).to(dt) if C1 else None
@@ -51,26 +59,25 @@ def main():
         def run():
             L.call("irx_op_conv2d", O.S(), O.DT[dt], O.P(x0), O.P(x1), C0, C1, N, H, W, H, W, O.P(wk), O.P(b), Co,
                    3, 3, 1, 1, 1, H, W, None, 0, None, O.P(out), 0, 0)
-        times = {d: [] for d in dbgs}
+        times = {n: [] for n, _ in sets}
         for _ in range(a.rounds):
-            for d in dbgs:
-                L.call("irx_set_option", b"gemm_dbg", d)
-                for _ in range(2):
-                    run()
-                torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.iters):
-                    run()
-                e1.record()
-                torch.cuda.synchronize()
-                times[d].append(e0.elapsed_time(e1) / a.iters * 1e3)
-        L.call("irx_set_option", b"gemm_dbg", 0)
-        base = statistics.median(times[0])
-        print(f"{lab}: {flops / base / 1e6:.0f} TF/s at dbg 0", flush=True)
-        for d in dbgs:
-            us = statistics.median(times[d])
-            print(f"  dbg {d:3d}: {us:8.1f} us  ({us / base:5.2f} x)", flush=True)
+            for n, opts in sets:
+                with L.option(**opts):
+                    for _ in range(2):
+                        run()
+                    torch.cuda.synchronize()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(a.iters):
+                        run()
+                    e1.record()
+                    torch.cuda.synchronize()
+                times[n].append(e0.elapsed_time(e1) / a.iters * 1e3)
+        base = statistics.median(times[sets[0][0]])
+        print(f"{lab}: {flops / base / 1e6:.0f} TF/s at {sets[0][0]}", flush=True)
+        for n, _ in sets:
+            us = statistics.median(times[n])
+            print(f"  {n:10s}: {us:8.1f} us  ({us / base:5.2f} x)  {flops / us / 1e6:6.0f} TF/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -43,12 +43,13 @@ def _dev(x, dt, device):
     return x.to(dt).to(device).contiguous()
 
 
-def produce(A, W, bias, R, dt, device):
+def produce(A, W, bias, R, dt, device, final_rs=False):
     M, K = A.shape
     N = W.shape[0]
     C = torch.empty(M, N, dtype=dt, device=device)
     parts = torch.full((M, N // 320, 2), float("nan"), dtype=torch.float32, device=device)
-    L.call("irx_op_gemm_ln_out", O.S(), O.DT[dt], M, N, K, O.P(A), O.P(W), O.P(bias), O.P(R), O.P(C), O.P(parts))
+    L.call("irx_op_gemm_ln_out", O.S(), O.DT[dt], M, N, K, O.P(A), O.P(W), O.P(bias), O.P(R), O.P(C), O.P(parts),
+           int(final_rs), 1e-5)
     return C, parts
 
 
@@ -99,6 +100,34 @@ def fold_gemm(x, Wg, u, v, dt, device, rs=None, parts=None, T=0, geglu=False):
     L.call("irx_op_gemm_ln_fold", O.S(), O.DT[dt], M, N, K, O.P(x), O.P(Wg), O.P(u), O.P(v), O.P(rs), O.P(parts),
            T, int(geglu), O.P(out))
     return out
+
+
+@pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("N,geglu", [(960, False), (320, False), (2560, True)])
+def test_ln_fold_from_producer_rs(device, dt, N, geglu):
+    """The engine's form at C = 320: the producer writes each row's final (rstd, rstd * mean) (final_rs), the folded
+    consumer takes it as its ln_rs — matching the statistics of the stored rows (fp64) and PyTorch LayerNorm +
+    projection."""
+    M, C = 8192, 320
+    A = _dev(_r(M, C, seed=40), dt, device)
+    Wp = _dev(_r(C, C, seed=41, scale=1 / math.sqrt(C)), dt, device)
+    h, rs = produce(A, Wp, _r(C, seed=42).to(device), _dev(_r(M, C, seed=43, shift=0.5), dt, device), dt, device,
+                    final_rs=True)
+    rs = rs.view(M, 2).contiguous()
+    hd = h.double()
+    mean = hd.mean(-1)
+    rstd = torch.rsqrt(((hd - mean[:, None]) ** 2).mean(-1) + 1e-5)
+    assert float(((rs[:, 0].double() - rstd).abs() / rstd).max()) < 2e-5
+    assert float(((rs[:, 1].double() - rstd * mean).abs() / (rstd * hd.abs().amax(-1))).max()) < 2e-5
+    W, b, gamma, beta = _ln_fold_operands(C, N, 44, geglu)
+    Wg, u, v = _fold(W, b, gamma, beta, dt, device, geglu)
+    got = fold_gemm(h, Wg, u, v, dt, device, rs=rs, geglu=geglu)
+    torch.cuda.synchronize()
+    ref = F.layer_norm(h.float().cpu(), (C,), gamma, beta, 1e-5) @ W.t() + b
+    if geglu:
+        hv, gt = ref.chunk(2, dim=-1)
+        ref = hv * F.gelu(gt)
+    assert O.rel_err(got, ref) < TOL[dt]
 
 
 @pytest.mark.parametrize("dt", DT16)
