@@ -76,7 +76,6 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"ln_parts", &g_ln_parts, nullptr},
     {"gn_fold", &g_gn_fold, nullptr},
     {"attn_pipe", &g_attn_pipe, nullptr},
-    {"halo_prio", &g_halo_prio, nullptr},
     {"halo_split", &g_halo_split, nullptr},
     {"halo_pipe", &g_halo_pipe, nullptr},
     {"gemm_pp", &g_gemm_pp, nullptr},

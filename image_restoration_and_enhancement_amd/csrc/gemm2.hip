@@ -371,20 +371,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         for (int j = 0; j < TN; ++j) fb[ss][j] = Bs[boff[ss] + j * 16 * CPR];
       }
     };
-    const bool pmma = (a.prio & 1) != 0;
     auto mma = [&]() {
       if (a.dbg & 2) return;
-      if (pmma) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
       for (int ss = 0; ss < KSUB; ++ss)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[ss][i], fb[ss][j], acc[i][j]);
-      if (pmma) {
-        if ((a.prio & 2) && g1) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-      }
     };
     const bool nobar = (a.dbg & 32) != 0;   // (timing diagnostics: no barriers)
     auto barrier = [&] {
@@ -406,7 +400,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       wait_vm((BAL ? BP0 : 0) + (c0 + 1 < cend ? HPG : 0));
     }
     barrier();                                           // (+ the zero row)
-    if ((a.prio & 2) && g1) __builtin_amdgcn_s_setprio(1);   // (static priority for the second-dispatched half)
     // one program for both groups: every wave runs {load phase of step k; barrier; compute phase of step k;
     // barrier}, group 1 one phase behind group 0 (one extra barrier in front, group 0 one extra at the end),
     // so each interval between barriers pairs one group's MFMAs with the other group's loads
@@ -450,7 +443,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       });
     }
     if (!g1) barrier();
-    if (a.prio) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   } else if constexpr (HALO == 1) {
@@ -779,7 +771,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       constexpr int CPR = BN / 8;               // 16-byte chunks per row
       // residual / row-add operands of the store passes requested before the first store (not for the 128x128 tiles:
       // two of them stay resident per CU only within 128 VGPRs)
-      constexpr bool kEpiPrefetch = !(BM == 128 && BN == 128) && NW == 8;
+      // (halo conv tiles only: the GroupNorm-partial loop of the 256x320 tiles spilled with it)
+      constexpr bool kEpiPrefetch = HALO != 0;
+      constexpr int kEpiPF = 4;
       // chunk swizzle inside whole groups of 8 chunks only (BN = 160 leaves a 4-chunk tail unswizzled)
       auto csw = [](int c, int row) { return c < (CPR & ~7) ? c ^ (row & 7) : c; };
       if (a.ln_rs || a.ln_part) {
@@ -791,23 +785,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           uu[j] = n < a.N ? a.ln_u[n] : 0.f;
           bb[j] = (biasp && n < a.N) ? biasp[n] : 0.f;
         }
-        // the four rows of accumulator block i + 1 are fetched (and merged) while block i is stored
-        float2 rsc[4], rsn[4];
-        auto fetch_rs = [&](int i, float2* dst) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = wm * TM * 16 + i * 16 + fgrp * 4 + r;
-            dst[r] = m0 + row < a.M ? ln_rs_at(a.ln_rs, a.ln_part, a.ln_T, a.ln_eps, m0 + row) : make_float2(0.f, 0.f);
-          }
-        };
-        fetch_rs(0, rsc);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          if (i + 1 < TM) fetch_rs(i + 1, rsn);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = wm * TM * 16 + i * 16 + fgrp * 4 + r;
-            const float2 rs = rsc[r];
+            const float2 rs = m0 + row < a.M ? ln_rs_at(a.ln_rs, a.ln_part, a.ln_T, a.ln_eps, m0 + row)
+                                             : make_float2(0.f, 0.f);
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
               const int col = wn * TN * 16 + j * 16 + frow;
@@ -815,9 +799,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
                   __builtin_bit_cast(uint16_t, from_f<T>(fmaf(acc[i][j][r], rs.x, fmaf(-rs.y, uu[j], bb[j]))));
             }
           }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) rsc[r] = rsn[r];
-        }
       } else {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -924,14 +905,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
             // per tile instead of one per row: the stores may alias the residual, so the compiler cannot hoist the
             // loads itself); the row add is one vector per image, loaded once when the tile lies in one image
             constexpr int KMAX = (BM + RS - 1) / RS;
-            uint4 rres[KMAX];
-            if (Rp) {
-#pragma unroll
-              for (int k = 0; k < KMAX; ++k) {
-                const int row = min(rg + k * RS, rend - 1);   // (clamped, not branched: one batch of loads)
-                rres[k] = *(const uint4*)(Rp + (long)(m0 + row) * a.ldr + n0 + cc * 8);
-              }
-            }
             const bool ra1 = a.rowadd && (m0 / a.rows_per_group) == ((m0 + rend - 1) / a.rows_per_group);
             float4 rx = make_float4(0.f, 0.f, 0.f, 0.f), ry = rx;
             if (ra1) {
@@ -939,13 +912,24 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
               rx = ra[0];
               ry = ra[1];
             }
+            // batches of kEpiPF rows: their residual loads issued together (clamped rows, no branches: one vmcnt)
+            uint4 rres[kEpiPF];
+#pragma unroll 1
+            for (int k0 = 0; k0 < KMAX; k0 += kEpiPF) {
+              if (Rp) {
 #pragma unroll
-            for (int k = 0; k < KMAX; ++k) {
-              const int row = rg + k * RS;
+                for (int u = 0; u < kEpiPF; ++u) {
+                  const int row = min(rg + (k0 + u) * RS, rend - 1);
+                  rres[u] = *(const uint4*)(Rp + (long)(m0 + row) * a.ldr + n0 + cc * 8);
+                }
+              }
+#pragma unroll
+            for (int u = 0; u < kEpiPF; ++u) {
+              const int row = rg + (k0 + u) * RS;
               if (row >= rend) break;
               Src q;
               q.u = *(const uint4*)(tileS + row * BN + (csw(cc, row) << 3));
-              q.r = rres[k];
+              q.r = rres[u];
               if (a.rowadd) {
                 if (ra1) {
                   q.x = rx;
@@ -958,6 +942,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
                 }
               }
               acc(combine(row, cc, q));
+            }
             }
           } else {
             // (one row per step: a two-row software pipeline here pushed the 128x128 tiles past 128 VGPRs,
@@ -1007,24 +992,30 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       // LayerNorm partials of the output (GemmArgs::ln_out; host: gemm_emits_ln_parts, BN == kLnGroup): the final
       // values are written back over the staged tile, then G threads per row reduce it in two passes
       float2* const lno = BN == kLnGroup ? a.ln_out : nullptr;
-      // residual chunks of all this thread's iterations requested up front (as in the GroupNorm-partial loop above)
-      constexpr int KIT = kEpiPrefetch ? (BM * CPR + NT - 1) / NT : 1;
-      uint4 rres[KIT];
-      if constexpr (kEpiPrefetch) {
-        if (Rp) {
+      // residual chunks requested kEpiPF iterations at a time (as in the GroupNorm-partial loop above)
+      // (the plain store pass keeps one chunk per step: prefetching here spilled the 256x320 tiles)
+      constexpr bool kPlainPF = false;
+      constexpr int KIT = kPlainPF ? (BM * CPR + NT - 1) / NT : 1;
+      constexpr int PF = kPlainPF ? kEpiPF : 1;
+      uint4 rres[PF];
+#pragma unroll 1
+      for (int k0 = 0; k0 < KIT; k0 += PF) {
+        if constexpr (kPlainPF) {
+          if (Rp) {
 #pragma unroll
-          for (int k = 0; k < KIT; ++k) {
-            const int idx = min(tid + k * NT, BM * CPR - 1);
-            const int row = idx / CPR, c = idx - row * CPR;
-            const int m = min(m0 + row, a.M - 1), n = min(n0 + c * 8, a.N - 8);
-            rres[k] = *(const uint4*)(Rp + (long)m * a.ldr + n);
+            for (int u = 0; u < PF; ++u) {
+              const int idx = min(tid + (k0 + u) * NT, BM * CPR - 1);
+              const int row = idx / CPR, c = idx - row * CPR;
+              const int m = min(m0 + row, a.M - 1), n = min(n0 + c * 8, a.N - 8);
+              rres[u] = *(const uint4*)(Rp + (long)m * a.ldr + n);
+            }
           }
         }
-      }
 #pragma unroll
-      for (int k = 0; k < KIT; ++k) {
+      for (int pu = 0; pu < PF; ++pu) {
+      const int k = k0 + pu;
 #pragma unroll 1
-      for (int idx = tid + k * NT; idx < BM * CPR; idx += (kEpiPrefetch ? BM * CPR : NT)) {
+      for (int idx = tid + k * NT; idx < BM * CPR; idx += (kPlainPF ? BM * CPR : NT)) {
         const int row = idx / CPR, c = idx - row * CPR;
         const int m = m0 + row, n = n0 + c * 8;
         if (m >= a.M || n >= a.N) continue;
@@ -1040,7 +1031,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           }
           if (Rp) {
             float rv[8];
-            Vec16<T>::unpack(kEpiPrefetch ? rres[k] : *(const uint4*)(Rp + (long)m * a.ldr + n), rv);
+            Vec16<T>::unpack(kPlainPF ? rres[pu] : *(const uint4*)(Rp + (long)m * a.ldr + n), rv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] += rv[e];
           }
@@ -1050,6 +1041,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           if (lno) *ts = u;
         }
         *(uint4*)(Cp + c_off(a, m, n)) = u;
+      }
       }
       }
       if constexpr (BN == kLnGroup && NT % BM == 0) {
@@ -1446,7 +1438,6 @@ size_t gemm_workspace_bytes(const GemmArgs& a) {
 // reduction) when two splits do, 0 = the halo path does not take the shape.
 int g_halo_split = 1;   // irx_set_option("halo_split", 0): no K-split halo tiles (A/B)
 int g_halo_pipe = 1;    // irx_set_option("halo_pipe", 0): the round-2 halo main loop (A/B)
-int g_halo_prio = 0;    // irx_set_option("halo_prio", m): ping-pong halo wave priorities (GemmArgs::prio; A/B)
 // irx_set_option("gemm_pp", 1): ping-pong main loop for dense GEMMs / im2col convs.  Off: measured slower at every
 // UNet / VAE shape (bench 553.8 vs 515.7 ms/step, the VAE 512x512 convs 1.9x; profiles/r03_kbench_*_pp.txt) — the
 // halo conv's gain came with its unrolled-tap addressing, which these loops do not need
@@ -1491,7 +1482,6 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     GemmArgs b = a;
     b.vec_epilogue = 1;
     b.dbg = g_gemm_dbg;
-    b.prio = g_halo_prio;
     Split sp;
     sp.per = a.K / 64;
     const int splits = halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));

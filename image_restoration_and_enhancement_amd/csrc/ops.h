@@ -79,8 +79,6 @@ struct GemmArgs {
   // (set by the launcher) N-major tile order: consecutive tiles (one XCD's range) share a B panel instead of an A
   // panel — for the weight-heavy small-M shapes (8x8-level convs: 29.5 MB of weights for 1024 rows)
   int nmajor = 0;
-  int prio = 0;           // (set by the launcher, halo conv) wave priority: 1 raised around each MFMA phase, 2 group 1
-                          // (waves 4-7) raised for the whole loop, 3 both (irx_set_option("halo_prio"), A/B)
   int dbg = 0;            // large-tile diagnostics (irx_set_option("gemm_dbg")): 1 skip epilogue, 2 skip MFMAs
 };
 constexpr int kCanonImages = 16;
@@ -165,7 +163,6 @@ extern int g_gemm_force;
 extern int g_conv_halo;      // 3x3 convs on whole-row tiles: one LDS halo per 32-channel slab for all 9 taps
 extern int g_gemm_pp;        // 1: ping-pong main loop for dense GEMMs (off: measured slower, see gemm2.hip)
 extern int g_halo_pipe;      // 1: software-pipelined halo main loop (fragments read one sub-step ahead)
-extern int g_halo_prio;      // ping-pong halo wave priorities (GemmArgs::prio)
 extern int g_halo_split;     // halo convs whose tiles alone do not fill the chip take two K splits
 extern int g_ln_stats8;    // LayerNorm statistics: 8 lanes per row (bit-identical to ln_kernel mode 2); 0 = A/B
 extern bool g_gn_v2;       // GroupNorm stats v3 (slabbed grid + finalize kernel); 0 = v1 (A/B)
