@@ -74,6 +74,12 @@ __device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds_addr) {
                : "memory", "m0");
 }
 
+// The same piece in the SADDR form: a wave-uniform 64-bit base (SGPRs) + a 32-bit per-lane byte offset.
+__device__ __forceinline__ void glds16_s(uint32_t voff, const void* base, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(base), "s"(lds_addr)
+               : "memory", "m0");
+}
+
 // BK: K depth of one LDS stage (64: 8 chunks of 16 B per row, 32: 4); S: stages in the ring.
 // S == 2 is the classic double buffer (drain + barrier per step); S > 2 keeps S-2 stages of LDS-DMA in
 // flight across each (raw) barrier, waiting with a counted vmcnt for exactly the stage about to be read.
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     }
   };
 
-  if constexpr (HALO == 2 || HALO == 3) {
+  if constexpr (HALO == 2 || HALO == 4) {
     // ---- ping-pong halo main loop (the default halo path; no GroupNorm-fused operand).  The two waves that
     //      share a SIMD (w and w + 4) take opposite roles in each half of a K step (slab c = kt / 9, tap
     //      t = kt % 9), so one of them always has MFMAs to issue while the other moves data:
@@ -257,21 +263,23 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     //                            previous phase; group 1 (waves 4-7) issues the LDS-DMA of B(kt + 2) and reads
     //                            its own fragments of step kt;
     //        phase 2 of step kt: group 1 runs its MFMAs of step kt; group 0 reads its fragments of step kt + 1
-    //                            and issues one sixth of a later slab's halo.
+    //                            and, at taps 0..5 of every slab c but the last, issues one sixth of slab c + 1's
+    //                            halo (into the buffer of slab c - 1, which every wave finished reading before the
+    //                            barrier that ended phase 1 of step 9c - 1... group 1's last load phase of c - 1).
     //      (the lock-step form, HALO == 1, issues DMA and fragment reads in both waves of a SIMD at once, and
     //      the matrix pipe idles meanwhile.)  B ring of S = 3 stages: B(kt + 2) goes into the stage of
-    //      step kt - 1, which group 1 finished reading before the barrier that ended phase 1 of kt - 1 and
-    //      group 0 before it ran step kt - 1's MFMAs; group 1 waits for B(kt + 1) at the end of phase 1 of
-    //      kt, where group 0 needs it.  Halo buffers: slab c + 2's halo is issued by group 0 in six parts in
-    //      phase 2 of steps 9c + 8 .. 9c + 13 (slab c's buffer is free once phase 1 of its last tap is over)
-    //      and waited for (vmcnt(0): group 0 issues nothing else) at the end of phase 1 of the step before
-    //      slab c + 2 starts.
-    static_assert(S == 3 && KSUB == 2 && NW == 8, "ping-pong halo: 3-stage B ring, BK 64, 8 waves");
-    // HALO == 3 (option halo_pipe 2): the B panel of a step is split between the groups — group 1 issues its first
-    // BP1 pieces per wave in its load phase (phase 1 of step kt - 2), group 0 the other BPG - BP1 in its own (phase 2
-    // of kt - 2, before that phase's halo pieces) — so neither load phase carries the whole panel's LDS-DMA issue
-    // (the lock-step loop above put all 5 pieces per wave in group 1's phase, 2 halo pieces in 6 of group 0's 9).
-    constexpr bool BAL = HALO == 3;
+    //      step kt - 1; group 1 waits for B(kt + 1) at the end of its load phase of kt, where group 0 needs it;
+    //      group 0 waits for slab c + 1's halo at the end of its compute phase of tap 8.
+    //      Each group runs its own straight-line program (9 taps unrolled, no role or diagnostic branches):
+    //      every DMA piece is one SADDR-form `global_load_lds_dwordx4` — a wave-uniform 64-bit source base in
+    //      SGPRs plus ONE per-lane byte offset (the XOR swizzle of a piece's 8 rows is the same for every piece,
+    //      RPI == 8), its LDS target a scalar add; the two B steps past the split's end are issued anyway, as
+    //      dummies into the free stage (in-range weight rows, never read), so every wait is a constant count.
+    //      HALO == 4: the same loop with the timing-diagnostic knock-outs of option gemm_dbg (bits 2 no MFMAs,
+    //      4 no B DMA, 8 no halo DMA, 16 no fragment reads, 32 no barriers; results are wrong when set).
+    static_assert(S == 3 && KSUB == 2 && NW == 8 && CPR == 8 && RPI == 8, "ping-pong halo: 3-stage B ring, BK 64");
+    constexpr bool DG = HALO == 4;
+    const int dbg = DG ? a.dbg : 0;
     const int W = a.g.Win, H = a.g.Hin, lw = __builtin_ctz(W);
     const int HW = H * W;
     const int img = m0 / HW, y0 = (m0 - img * HW) >> lw;
@@ -282,53 +290,64 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     static_assert(HPG * RPI * NG == BM + 2 * kHaloWMax && HPP * HPARTS == HPG, "halo pieces");
     constexpr int NBI = BN / RPI, BPG = NBI / NG;          // B wave-instructions per step, per group-1 wave
     static_assert(BPG * NG == NBI, "B pieces");
-    constexpr int BP1 = BAL ? (BPG + 1) / 2 : BPG, BP0 = BPG - BP1;   // per wave: group 1's / group 0's pieces
-    const int wv = __builtin_amdgcn_readfirstlane(wave);   // (scalar: the role branches stay uniform)
+    const int wv = __builtin_amdgcn_readfirstlane(wave);   // (scalar: the role branch stays uniform)
     const bool g1 = wv >= NG;
     const int gw = wv - (g1 ? NG : 0);
     uint4* const Hb = smem;                           // [2][HB_U4]
     uint4* const Bsm = smem + 2 * HB_U4;              // [S][BN * CPR]
     uint4* const zrow = Bsm + S * BN * CPR;           // one zero pixel row: taps left / right of the image
-    uint4* const scratch = zrow + CPR;                // 1 KiB target of the surplus pieces
+    uint4* const scratch = zrow + CPR;                // 1 KiB target of the surplus / out-of-image pieces
     if (tid < CPR) zrow[tid] = uint4{0u, 0u, 0u, 0u};
-    auto swz = [](int r) { return CPR == 8 ? (r & 7) : (((r >> 2) & 1) << 1); };
-    const uint16_t* bro[BPG];
-#pragma unroll
-    for (int j = 0; j < BPG; ++j) {
-      const int q = gw * BPG + j, r = RPI * q + lane / CPR;
-      bro[j] = n0 + r < a.N ? Bp + (long)(n0 + r) * a.ldb + (((lane % CPR) ^ swz(r)) * 8) : nullptr;
-    }
-    // pieces [j0, j1) of this wave's BPG-piece share of B(kt) (group 1: [0, BP1), group 0: [BP1, BPG))
-    auto issueB = [&](int kt, auto j0c, auto j1c) {
-      constexpr int j0 = decltype(j0c)::value, j1 = decltype(j1c)::value;
-      if (a.dbg & 4) return;      // (timing diagnostics: no B DMA)
-      const int c = kt / 9, t = kt - 9 * c;
-      const int off = t * Cin + c * BK;
-      uint4* const st = Bsm + (kt % S) * BN * CPR;
-#pragma unroll
-      for (int j = j0; j < j1; ++j) {
-        uint4* dst = st + (gw * BPG + j) * 64;
-        glds16_asm(bro[j] ? bro[j] + off : zp, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)smem);
+    const uint32_t ldsX = lds0 + (uint32_t)(scratch - smem) * 16u;
+    // lane -> (row lr of the piece's 8, 16-byte chunk slot); the slot holds logical chunk slot ^ lr (= row & 7)
+    const int lr = lane >> 3, lch = (lane & 7) ^ lr;
+    // ---- halo rows outside the image (top / bottom tiles): zero in both buffers once, never DMA'd
+    {
+      const int ylo = y0 - 1, yhi = y0 + (BM >> lw);   // the halo's first / last image row
+      for (int i = tid; i < 2 * (W * CPR); i += NT) {
+        const int side = i / (W * CPR), k = i - side * (W * CPR);
+        const bool out = side == 0 ? ylo < 0 : yhi >= H;
+        const int hrow = side == 0 ? 0 : (BM >> lw) + 1;
+        if (out) {
+          Hb[hrow * W * CPR + k] = uint4{0u, 0u, 0u, 0u};
+          Hb[HB_U4 + hrow * W * CPR + k] = uint4{0u, 0u, 0u, 0u};
+        }
       }
+    }
+    // group 1: B(kt) pieces j = 0 .. BPG-1 of this wave: weight rows n0 + RPI * (gw * BPG + j) + lr
+    const uint32_t voffB = (uint32_t)(lr * a.ldb + lch * 8) * 2u;
+    const char* const bB = (const char*)(Bp + (long)(n0 + RPI * gw * BPG) * a.ldb);
+    const long pstrB = (long)RPI * a.ldb * 2;
+    const uint32_t ldsB = lds0 + (uint32_t)(2 * HB_U4 + gw * BPG * 64) * 16u;
+    auto issueB = [&](int c, auto tc, int st) {   // B of (slab c, tap t) into stage st
+      constexpr int t = decltype(tc)::value;
+      if (DG && (dbg & 4)) return;
+      const char* b = bB + (long)(t * Cin + c * BK) * 2;
+      const uint32_t m = ldsB + (uint32_t)st * (BN * CPR * 16);
+#pragma unroll
+      for (int j = 0; j < BPG; ++j) glds16_s(voffB, b + j * pstrB, m + j * 1024u);
     };
-    using I0 = std::integral_constant<int, 0>;
-    using IP1 = std::integral_constant<int, BP1>;
-    using IPG = std::integral_constant<int, BPG>;
-    auto issueH = [&](int c, int j0, int j1) {   // group 0: pieces [j0, j1) of slab c's halo
-      if (a.dbg & 8) return;      // (timing diagnostics: no halo DMA)
+    // group 0: halo piece q = gw * HPG + j of slab c = pixels RPI * q .. + 7 of the (rows + 2) x W halo, which
+    // starts at image pixel P0 = (img * H + y0 - 1) * W; a piece is wholly inside or outside the image
+    const long P0 = (long)(img * H + y0 - 1) * W;
+    const long Plo = (long)img * HW, Phi = Plo + HW;
+    const uint32_t voffH0 = (uint32_t)(lr * a.g.C0 + lch * 8) * 2u;
+    const uint32_t voffH1 = (uint32_t)(lr * a.g.C1 + lch * 8) * 2u;
+    auto issueH = [&](int c, int j0, int j1) {    // pieces [j0, j1) of slab c's halo
+      if (DG && (dbg & 8)) return;
       const bool second = c * BK >= a.g.C0;
-      const uint16_t* sb = second ? (const uint16_t*)a.g.src1 : (const uint16_t*)a.g.src0;
+      const char* sb = (const char*)(second ? a.g.src1 : a.g.src0);
       const int cs = second ? a.g.C1 : a.g.C0;
       const int ch = second ? c * BK - a.g.C0 : c * BK;
-#pragma unroll 1
+      const uint32_t vo = second ? voffH1 : voffH0;
+      const uint32_t mb = lds0 + (uint32_t)((c & 1) * HB_U4) * 16u;
+#pragma unroll
       for (int j = j0; j < j1; ++j) {
         const int q = gw * HPG + j;
-        const int p = RPI * q + lane / CPR;
-        const int y = y0 - 1 + (p >> lw), x = p & (W - 1);
-        const bool ok = q < nhi && y >= 0 && y < H;
-        const uint16_t* src = ok ? sb + ((long)(img * H + y) * W + x) * cs + ch + (((lane % CPR) ^ swz(p)) * 8) : zp;
-        uint4* dst = q < nhi ? Hb + (c & 1) * HB_U4 + q * 64 : scratch;
-        glds16_asm(src, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
+        const long P = P0 + RPI * q;
+        const bool ok = q < nhi && P >= Plo && P < Phi;
+        glds16_s(vo, ok ? sb + (P * cs + ch) * 2 : sb, ok ? mb + (uint32_t)q * 1024u : ldsX);
       }
     };
     // ---- fragment addressing, hoisted out of the K loop.  With the 9 taps of a slab unrolled, the tap (ky, kx)
@@ -355,7 +374,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     uint4 fa[KSUB][TM], fb[KSUB][TN];
     auto readF = [&](auto tc, const uint4* Hs) {   // this wave's fragments of tap t (both 32-deep sub-steps)
       constexpr int t = decltype(tc)::value, ky = t / 3, kx = t % 3, st = t % S;
-      if (a.dbg & 16) return;     // (timing diagnostics: no fragment reads)
+      if (DG && (dbg & 16)) return;
       const uint4* Bs = Bsm + st * BN * CPR + bwave;
       const uint4* Hrow = Hs + awave + ky * rowW + (kx - 1) * CPR;
 #pragma unroll
@@ -372,7 +391,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       }
     };
     auto mma = [&]() {
-      if (a.dbg & 2) return;
+      if (DG && (dbg & 2)) return;
 #pragma unroll
       for (int ss = 0; ss < KSUB; ++ss)
 #pragma unroll
@@ -380,69 +399,56 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[ss][i], fb[ss][j], acc[i][j]);
     };
-    const bool nobar = (a.dbg & 32) != 0;   // (timing diagnostics: no barriers)
     auto barrier = [&] {
-      if (nobar) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (DG && (dbg & 32)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
-    // this split's K steps [kt0, nk): whole slabs (host: sp.per is a multiple of 9); >= 9 steps per split
-    const int nk = kt1, c0 = kt0 / 9, cend = (kt1 + 8) / 9;
+    // this split's K steps [kt0, kt1): whole slabs (host: sp.per is a multiple of 9); >= 9 steps per split
+    const int c0 = kt0 / 9, cend = (kt1 + 8) / 9;
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
     if (g1) {
-      issueB(kt0, I0{}, IP1{});
-      issueB(kt0 + 1, I0{}, IP1{});
-      wait_vm(BP1);                                      // B(kt0) landed
+      issueB(c0, I0{}, 0);
+      issueB(c0, I1{}, 1);
+      wait_vm(BPG);                                      // B(kt0) landed
+      barrier();                                         // (+ the zero row, the zeroed out-of-image halo rows)
+      barrier();                                         // group 1 runs one phase behind group 0
+      for (int c = c0; c < cend; ++c) {
+        const uint4* Hs = Hb + (c & 1) * HB_U4;
+        static_for(std::make_integer_sequence<int, 9>{}, [&](auto tc) {
+          constexpr int t = decltype(tc)::value;
+          // load phase: B(kt + 2) (past the split's end: a dummy), fragments of kt, B(kt + 1) landed
+          if constexpr (t < 7) issueB(c, std::integral_constant<int, t + 2>{}, (t + 2) % S);
+          else issueB(c + 1, std::integral_constant<int, t - 7>{}, (t + 2) % S);
+          readF(tc, Hs);
+          wait_vm(BPG);
+          barrier();
+          mma();                                         // compute phase
+          barrier();
+        });
+      }
     } else {
-      if constexpr (BAL) issueB(kt0, IP1{}, IPG{});
       issueH(c0, 0, HPG);
-      if constexpr (BAL) issueB(kt0 + 1, IP1{}, IPG{});
-      if (c0 + 1 < cend) issueH(c0 + 1, 0, HPG);
-      // B(kt0) and H(c0) landed (group 0's part of B(kt0 + 1) is waited for in its first compute phase)
-      wait_vm((BAL ? BP0 : 0) + (c0 + 1 < cend ? HPG : 0));
-    }
-    barrier();                                           // (+ the zero row)
-    // one program for both groups: every wave runs {load phase of step k; barrier; compute phase of step k;
-    // barrier}, group 1 one phase behind group 0 (one extra barrier in front, group 0 one extra at the end),
-    // so each interval between barriers pairs one group's MFMAs with the other group's loads
-    if (g1) barrier();
-    for (int c = c0; c < cend; ++c) {
-      const uint4* Hs = Hb + (c & 1) * HB_U4;
-      const bool last = c + 1 == cend;
-      const bool halo_next = c > c0 && !last;            // group 0 streams slab c + 1's halo at taps 0..5
-      static_for(std::make_integer_sequence<int, 9>{}, [&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        const int kt = 9 * c + t;
-        // ---- load phase
-        if (g1) {
-          if (!(last && t >= 7)) issueB(kt + 2, I0{}, IP1{});
-        } else {
-          if constexpr (BAL) {
-            if (!(last && t >= 7)) issueB(kt + 2, IP1{}, IPG{});
+      wait_vm(0);                                        // H(c0) landed
+      barrier();
+      for (int c = c0; c < cend; ++c) {
+        const uint4* Hs = Hb + (c & 1) * HB_U4;
+        const bool more = c + 1 < cend;
+        static_for(std::make_integer_sequence<int, 9>{}, [&](auto tc) {
+          constexpr int t = decltype(tc)::value;
+          // load phase: a sixth of slab c + 1's halo, fragments of kt (B(kt) landed: group 1 waited for it)
+          if constexpr (t < HPARTS) {
+            if (more) issueH(c + 1, t * HPP, (t + 1) * HPP);
           }
-          if (t < HPARTS && halo_next) issueH(c + 1, t * HPP, (t + 1) * HPP);
-        }
-        readF(tc, Hs);
-        if (g1 && !(last && t == 8)) {                   // B(kt + 1) landed (group 0 reads it next)
-          if (last && t == 7) wait_vm(0);
-          else wait_vm(BP1);
-        }
-        barrier();
-        // ---- compute phase
-        mma();
-        if (!g1) {
-          if (t == 8 && !last) {
-            wait_vm(0);                                  // the next slab's halo landed (and B(kt + 1))
-          } else if constexpr (BAL) {
-            // group 0's part of B(kt + 1), issued in its previous load phase before that phase's halo pieces
-            const int hprev = t == 0 ? (c == c0 && c0 + 1 < cend ? HPG : 0)
-                                     : ((t - 1) < HPARTS && halo_next ? HPP : 0);
-            wait_vm(hprev);
-          }
-        }
-        barrier();
-        (void)kt;
-      });
+          readF(tc, Hs);
+          barrier();
+          mma();                                         // compute phase
+          if constexpr (t == 8) wait_vm(0);              // slab c + 1's halo landed
+          barrier();
+        });
+      }
+      barrier();
     }
-    if (!g1) barrier();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   } else if constexpr (HALO == 1) {
@@ -1191,7 +1197,8 @@ void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
 
 template <int BM, int BN, int WM, int WN, int BK, int S, int HALO = 0, bool PP = false>
 void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
-  if (a.dtype == F16) launch2_t<f16_t, BM, BN, WM, WN, BK, S, HALO, PP>(a, sp, s);
+  if constexpr (HALO == 4) launch2_t<bf16_t, BM, BN, WM, WN, BK, S, HALO, PP>(a, sp, s);   // (bf16 diagnostics only)
+  else if (a.dtype == F16) launch2_t<f16_t, BM, BN, WM, WN, BK, S, HALO, PP>(a, sp, s);
   else launch2_t<bf16_t, BM, BN, WM, WN, BK, S, HALO, PP>(a, sp, s);
 }
 
@@ -1496,7 +1503,7 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
       sp.inkernel = true;
       sp.cnt = stream_counters(s);
     }
-    if (g_halo_pipe == 2 && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 3>(b, sp, s);   // ping-pong, B split by group
+    if (g_halo_pipe && !a.gn_ab && b.dbg && a.dtype == BF16) launch2<256, 160, 4, 2, 64, 3, 4>(b, sp, s);   // (diagnostics)
     else if (g_halo_pipe && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 2>(b, sp, s);   // ping-pong main loop
     else launch2<256, 160, 4, 2, 64, 3, 1>(b, sp, s);
     return true;
