@@ -70,12 +70,12 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gemm_deep", &g_gemm_deep, nullptr},
     {"gemm_dbg", &g_gemm_dbg, nullptr},
     {"gn_v2", nullptr, &g_gn_v2},
-    {"ln_stats8", &g_ln_stats8, nullptr},
     {"gn_fuse", &g_gn_fuse, nullptr},
     {"gn_parts", &g_gn_parts, nullptr},
     {"ln_parts", &g_ln_parts, nullptr},
     {"gn_fold", &g_gn_fold, nullptr},
     {"attn_pipe", &g_attn_pipe, nullptr},
+    {"attn_pf", &g_attn_pf, nullptr},
     {"halo_split", &g_halo_split, nullptr},
     {"halo_pipe", &g_halo_pipe, nullptr},
     {"gemm_pp", &g_gemm_pp, nullptr},

@@ -28,6 +28,15 @@
 namespace irx {
 
 __device__ uint4 g_zero_page[4];   // 64 zero bytes: the source of every padded / out-of-range lane
+#ifdef IRX_HALO_STAMPS
+constexpr int kHaloStampBlocks = 2048;
+__device__ unsigned long long g_halo_stamps[kHaloStampBlocks * 8 * 8];
+// (timing-diagnostic build) per (block, wave): 5 segment sums of the halo loop's taps + the tap count
+extern "C" int irx_debug_halo_stamps(void* out, int n) {
+  if (n > kHaloStampBlocks * 64) n = kHaloStampBlocks * 64;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_halo_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+}
+#endif
 
 namespace {
 
@@ -399,10 +408,30 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[ss][i], fb[ss][j], acc[i][j]);
     };
+    // (sched_barrier: the MFMAs touch no memory, so without it the scheduler hoists them across the barrier asm
+    // into the load phase, right behind the fragment reads they use — one wave then runs loads and MFMAs in
+    // series and the two groups no longer alternate)
     auto barrier = [&] {
+      __builtin_amdgcn_sched_barrier(0);
       if (DG && (dbg & 32)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
     };
+    // timing-diagnostic build only (-DIRX_HALO_STAMPS, HALO == 4): per wave, scalar sums of the cycles between
+    // the stamps of every tap (0 -> 1 DMA issue + fragment reads landed, 1 -> 2 B wait, 2 -> 3 barrier after the load
+    // phase, 3 -> 4 MFMA issue, 4 -> 5 barrier after the compute phase), stored once by lane 0 into g_halo_stamps
+#ifdef IRX_HALO_STAMPS
+    unsigned long long stv[6] = {0, 0, 0, 0, 0, 0}, sts[5] = {0, 0, 0, 0, 0};
+#define IRX_STAMP(i)                                                                                  \
+  if constexpr (DG) {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stv[i])::"memory");                   \
+    __builtin_amdgcn_sched_barrier(0);                                                                \
+    if constexpr (i > 0) sts[i - 1] += stv[i] - stv[i - 1];                                          \
+  }
+#else
+#define IRX_STAMP(i)
+#endif
     // this split's K steps [kt0, kt1): whole slabs (host: sp.per is a multiple of 9); >= 9 steps per split
     const int c0 = kt0 / 9, cend = (kt1 + 8) / 9;
     using I0 = std::integral_constant<int, 0>;
@@ -418,13 +447,19 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         static_for(std::make_integer_sequence<int, 9>{}, [&](auto tc) {
           constexpr int t = decltype(tc)::value;
           // load phase: B(kt + 2) (past the split's end: a dummy), fragments of kt, B(kt + 1) landed
+          IRX_STAMP(0);
           if constexpr (t < 7) issueB(c, std::integral_constant<int, t + 2>{}, (t + 2) % S);
           else issueB(c + 1, std::integral_constant<int, t - 7>{}, (t + 2) % S);
           readF(tc, Hs);
+          IRX_STAMP(1);
           wait_vm(BPG);
+          IRX_STAMP(2);
           barrier();
+          IRX_STAMP(3);
           mma();                                         // compute phase
+          IRX_STAMP(4);
           barrier();
+          IRX_STAMP(5);
         });
       }
     } else {
@@ -437,18 +472,35 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         static_for(std::make_integer_sequence<int, 9>{}, [&](auto tc) {
           constexpr int t = decltype(tc)::value;
           // load phase: a sixth of slab c + 1's halo, fragments of kt (B(kt) landed: group 1 waited for it)
+          IRX_STAMP(0);
           if constexpr (t < HPARTS) {
             if (more) issueH(c + 1, t * HPP, (t + 1) * HPP);
           }
           readF(tc, Hs);
+          IRX_STAMP(1);
+          IRX_STAMP(2);
           barrier();
+          IRX_STAMP(3);
           mma();                                         // compute phase
           if constexpr (t == 8) wait_vm(0);              // slab c + 1's halo landed
+          IRX_STAMP(4);
           barrier();
+          IRX_STAMP(5);
         });
       }
       barrier();
     }
+#ifdef IRX_HALO_STAMPS
+    if constexpr (DG) {
+      if (lane == 0 && blockIdx.x < kHaloStampBlocks) {
+        unsigned long long* o = g_halo_stamps + ((long)blockIdx.x * NW + wave) * 8;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) o[i] = sts[i];
+        o[5] = (unsigned long long)(cend - c0) * 9;
+      }
+    }
+#endif
+#undef IRX_STAMP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   } else if constexpr (HALO == 1) {

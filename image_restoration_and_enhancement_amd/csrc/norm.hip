@@ -404,71 +404,6 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, long l
   }
 }
 
-// LayerNorm statistics only, 16-bit rows, 8 lanes per row (8 rows per wave): the same numbers as ln_kernel mode 2
-// bit for bit.  ln_kernel's lane l sums chunks l, l + 64, ... (8 elements each, in order) and then reduces over the 64
-// lanes by the xor butterfly 32, 16, 8, 4, 2, 1; here lane g of a row's group plays the virtual lanes 8j + g (j < 8):
-// levels 32 / 16 / 8 pair virtual lanes of the same g (in registers), levels 4 / 2 / 1 are shuffles within the group.
-// Every 16-byte load of the wave covers 8 rows x 128 contiguous bytes, no idle lanes at C = 320.
-template <typename T, int MAXV>
-__global__ __launch_bounds__(256) void ln_stats8_kernel(const T* __restrict__ x, long ldx, int rows, int C, float eps,
-                                                        float2* __restrict__ stats) {
-  constexpr int VEC = 8;
-  static_assert(sizeof(T) == 2, "16-bit rows");
-  const int lane = threadIdx.x & 63, g = lane & 7;
-  const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (lane >> 3);
-  const bool live = row < rows;
-  const int nv = C / VEC;
-  uint4 raw[8][MAXV];
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      const int v = 8 * j + g + 64 * i;
-      raw[j][i] = (live && v < nv) ? *(const uint4*)(x + (long)row * ldx + v * VEC) : make_uint4(0, 0, 0, 0);
-    }
-  auto butterfly = [&](float* t) {   // t[j] = virtual lane 8j + g
-#pragma unroll
-    for (int o = 4; o > 0; o >>= 1)
-#pragma unroll
-      for (int j = 0; j < o; ++j) t[j] += t[j + o];
-    float r = t[0];
-#pragma unroll
-    for (int o = 4; o > 0; o >>= 1) r += __shfl_xor(r, o);
-    return r;
-  };
-  float t[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < MAXV; ++i)
-      if (8 * j + g + 64 * i < nv) {
-        float f[VEC];
-        Vec16<T>::unpack(raw[j][i], f);
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) s += f[e];
-      }
-    t[j] = s;
-  }
-  const float mean = butterfly(t) / C;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < MAXV; ++i)
-      if (8 * j + g + 64 * i < nv) {
-        float f[VEC];
-        Vec16<T>::unpack(raw[j][i], f);
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) { const float dd = f[e] - mean; q = fmaf(dd, dd, q); }
-      }
-    t[j] = q;
-  }
-  const float q = butterfly(t);
-  const float rstd = rsqrtf(q / C + eps);
-  if (live && g == 0) stats[row] = make_float2(rstd, rstd * mean);
-}
-
 constexpr int kMaxC = 8192;
 
 // statistics of the (two-source) tensor -> per-channel scale / shift `ab` [N][C]
@@ -562,17 +497,6 @@ void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamm
       throw Error("layer_norm: C too large");
     }
   };
-  if constexpr (sizeof(T) == 2) {
-    if (stats && g_ln_stats8 && nv <= 192) {
-      ProfScope ps8(prof_on() ? std::string("irx::(anonymous namespace)::ln_stats8_kernel") : std::string(), 0.0, s);
-      const dim3 g8((rows + 31) / 32);
-      if (nv <= 64) ln_stats8_kernel<T, 1><<<g8, block, 0, s>>>((const T*)x, ldx, rows, C, eps, stats);
-      else if (nv <= 128) ln_stats8_kernel<T, 2><<<g8, block, 0, s>>>((const T*)x, ldx, rows, C, eps, stats);
-      else ln_stats8_kernel<T, 3><<<g8, block, 0, s>>>((const T*)x, ldx, rows, C, eps, stats);
-      IRX_LAUNCH_CHECK();
-      return;
-    }
-  }
   if (stats) launch(std::integral_constant<int, 2>{});
   else if (gamma) launch(std::integral_constant<int, 0>{});
   else launch(std::integral_constant<int, 1>{});
@@ -629,7 +553,6 @@ void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* 
   IRX_LAUNCH_CHECK();
 }
 
-int g_ln_stats8 = 0;   // irx_set_option("ln_stats8", 1): LayerNorm statistics 8 lanes per row (A/B; off until measured on the GPU)
 bool g_gn_v2 = true;   // irx_set_option("gn_v2", 0): v1 LDS-atomic stats + separate finalize (A/B)
 
 size_t gn_ws_bytes(int N, int HW, int G) {

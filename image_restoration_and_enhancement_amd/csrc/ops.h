@@ -164,7 +164,6 @@ extern int g_conv_halo;      // 3x3 convs on whole-row tiles: one LDS halo per 3
 extern int g_gemm_pp;        // 1: ping-pong main loop for dense GEMMs (off: measured slower, see gemm2.hip)
 extern int g_halo_pipe;      // 1: software-pipelined halo main loop (fragments read one sub-step ahead)
 extern int g_halo_split;     // halo convs whose tiles alone do not fill the chip take two K splits
-extern int g_ln_stats8;    // LayerNorm statistics: 8 lanes per row (bit-identical to ln_kernel mode 2); 0 = A/B
 extern bool g_gn_v2;       // GroupNorm stats v3 (slabbed grid + finalize kernel); 0 = v1 (A/B)
 void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
                 const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s);
@@ -213,6 +212,7 @@ struct AttnArgs {
 void attention(const AttnArgs& a, hipStream_t s);
 extern bool g_attn_v2;
 extern int g_attn_v3;    // 32x32x16 kernel for bf16 / fp16 (0: the round-1 kernels, bf16 only)
+extern int g_attn_pf;    // 1: non-causal streamed d = 40 attention with whole-tile K / V fragment prefetch (attn3 PF)
 extern int g_attn_pipe;  // 1: non-causal streamed d = 40 attention with QK^T one key tile ahead (attn3p)
 extern int g_attn_prio;
 extern int g_attn_qrep;

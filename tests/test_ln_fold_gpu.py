@@ -50,23 +50,3 @@ def test_unet_ln_fold(device, dtype, h, w, B):
     assert rel(folded, plain) < tol_ab, rel(folded, plain)
     print(f"\nln_fold {dtype} {h}x{w}: vs oracle {rel(folded, ref):.3e} (unfolded {rel(plain, ref):.3e}), "
           f"folded vs unfolded {rel(folded, plain):.3e}")
-
-
-@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
-@pytest.mark.parametrize("h,w,B", [(32, 32, 4), (64, 64, 2), (7, 5, 2)])
-def test_ln_stats8_bit_exact(device, dtype, h, w, B):
-    """The 8-lanes-per-row LayerNorm statistics kernel (option ln_stats8) reproduces ln_kernel's per-lane sums and
-    64-lane butterfly: the folded UNet's output is identical with it on and off (C = 320 / 640 / 1280 rows, odd row
-    counts at 7x5)."""
-    pc, sd = MC.state_dicts("denoise")
-    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
-    g = torch.Generator().manual_seed(12)
-    x = torch.randn(B, 4, h, w, generator=g)
-    ctx = torch.randn(B, 77, 768, generator=g)
-    u = _unet(pc, sd, dtype, device, True)
-    outs = []
-    for v in (1, 0):
-        with L.option(ln_stats8=v):
-            outs.append(_run(u, x, ctx, 481, tdt, device).float().cpu())
-    assert torch.isfinite(outs[0]).all()
-    assert torch.equal(outs[0], outs[1])

@@ -723,3 +723,20 @@ def test_attention_pipelined_d40(device, dt, B, Lq, Lk):
     assert O.rel_err(got, base.float()) < (1e-2 if dt == torch.bfloat16 else 2e-3)
     ref = O.ref_attention(_q(q[:1], dt), _q(k[:1], dt), _q(v[:1], dt), heads)
     assert O.rel_err(got[:1], ref) < 2 * TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("B,Lq,Lk", [(2, 1024, 1024), (1, 333, 190), (1, 64, 129), (2, 4096, 4096)])
+def test_attention_prefetch_d40_bit_exact(device, dt, B, Lq, Lk):
+    """attn3 with whole-tile K / V fragment prefetch (option attn_pf) issues the same MFMAs on the same operands in the
+    same order as the default kernel — only the LDS reads move — so the outputs are identical bit for bit."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    C, heads = 320, 8
+    q, k, v = _r(B, Lq, C, seed=73) * 2, _r(B, Lk, C, seed=74) * 2, _r(B, Lk, C, seed=75)
+    qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
+    with L.option(attn_pf=1):
+        got = O.attention(qd, kd, vd, heads)
+    with L.option(attn_pf=0):
+        base = O.attention(qd, kd, vd, heads)
+    torch.cuda.synchronize()
+    assert torch.equal(got, base)
