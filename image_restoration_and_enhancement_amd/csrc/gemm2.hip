@@ -399,6 +399,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         for (int j = 0; j < TN; ++j) fb[ss][j] = Bs[boff[ss] + j * 16 * CPR];
       }
     };
+    auto prio = [&](bool load) {   // (diagnostics only: bit 128 load phases at priority 1, bit 256 compute phases)
+      if constexpr (DG) {
+        if (dbg & (load ? 128 : 256)) __builtin_amdgcn_s_setprio(1);
+        else if (dbg & 384) __builtin_amdgcn_s_setprio(0);
+      }
+    };
     auto mma = [&]() {
       if (DG && (dbg & 2)) return;
 #pragma unroll
@@ -448,6 +454,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           constexpr int t = decltype(tc)::value;
           // load phase: B(kt + 2) (past the split's end: a dummy), fragments of kt, B(kt + 1) landed
           IRX_STAMP(0);
+          prio(true);
           if constexpr (t < 7) issueB(c, std::integral_constant<int, t + 2>{}, (t + 2) % S);
           else issueB(c + 1, std::integral_constant<int, t - 7>{}, (t + 2) % S);
           readF(tc, Hs);
@@ -456,6 +463,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           IRX_STAMP(2);
           barrier();
           IRX_STAMP(3);
+          prio(false);
           mma();                                         // compute phase
           IRX_STAMP(4);
           barrier();
@@ -473,6 +481,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           constexpr int t = decltype(tc)::value;
           // load phase: a sixth of slab c + 1's halo, fragments of kt (B(kt) landed: group 1 waited for it)
           IRX_STAMP(0);
+          prio(true);
           if constexpr (t < HPARTS) {
             if (more) issueH(c + 1, t * HPP, (t + 1) * HPP);
           }
@@ -481,6 +490,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           IRX_STAMP(2);
           barrier();
           IRX_STAMP(3);
+          prio(false);
           mma();                                         // compute phase
           if constexpr (t == 8) wait_vm(0);              // slab c + 1's halo landed
           IRX_STAMP(4);

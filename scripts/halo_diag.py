@@ -86,6 +86,10 @@ def main():
             print(f"  {n:10s}: {us:8.1f} us  ({us / base:5.2f} x)  {flops / us / 1e6:6.0f} TF/s", flush=True)
 
 
+DBG_STAMPS = [(0, "as is"), (2, "no MFMAs"), (12, "no DMA"), (16, "no fragment reads"), (128, "load phases prio 1"),
+              (256, "compute phases prio 1")]
+
+
 def stamps():
     import ctypes
     import numpy as np
@@ -100,23 +104,24 @@ def stamps():
         wk = (torch.randn(Co, 3, 3, C0 + C1, device=dev, generator=g) / math.sqrt(9 * (C0 + C1))).to(dt)
         b = torch.zeros(Co, device=dev)
         out = torch.empty(N, H, W, Co, dtype=dt, device=dev)
-        with L.option(gemm_dbg=64):   # (bit 64: the HALO == 4 instantiation, nothing knocked out)
-            for _ in range(20):
-                L.call("irx_op_conv2d", O.S(), O.DT[dt], O.P(x0), O.P(x1), C0, C1, N, H, W, H, W, O.P(wk), O.P(b), Co,
-                       3, 3, 1, 1, 1, H, W, None, 0, None, O.P(out), 0, 0)
-            torch.cuda.synchronize()
-        nblk = min(2048, N * H * W // 256 * (Co // 160) * (2 if "split 2" in lab else 1))
-        buf = np.zeros(nblk * 64, dtype=np.uint64)
-        fn = L.load().irx_debug_halo_stamps
-        fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
-        fn(buf.ctypes.data, buf.size)
-        st = buf.reshape(nblk, 8, 8).astype(np.float64)
-        taps = st[:, :, 5]
-        print(f"{lab}: cycles per tap (mean over {nblk} blocks)", flush=True)
-        for grp, ws in (("group 0 (halo)", slice(0, 4)), ("group 1 (B)", slice(4, 8))):
-            per = st[:, ws, :5].sum(axis=(0, 1)) / taps[:, ws].sum()
-            print(f"  {grp:15s} " + "  ".join(f"{n}: {v:6.0f}" for n, v in zip(seg, per)) +
-                  f"  | total {per.sum():6.0f}", flush=True)
+        for dbg, what in DBG_STAMPS:
+            with L.option(gemm_dbg=64 | dbg):   # (bit 64: the HALO == 4 instantiation; + knock-out / priority bits)
+                for _ in range(20):
+                    L.call("irx_op_conv2d", O.S(), O.DT[dt], O.P(x0), O.P(x1), C0, C1, N, H, W, H, W, O.P(wk), O.P(b),
+                           Co, 3, 3, 1, 1, 1, H, W, None, 0, None, O.P(out), 0, 0)
+                torch.cuda.synchronize()
+            nblk = min(2048, N * H * W // 256 * (Co // 160) * (2 if "split 2" in lab else 1))
+            buf = np.zeros(nblk * 64, dtype=np.uint64)
+            fn = L.load().irx_debug_halo_stamps
+            fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
+            fn(buf.ctypes.data, buf.size)
+            st = buf.reshape(nblk, 8, 8).astype(np.float64)
+            taps = st[:, :, 5]
+            print(f"{lab} [{what}]: cycles per tap (mean over {nblk} blocks)", flush=True)
+            for grp, ws in (("group 0 (halo)", slice(0, 4)), ("group 1 (B)", slice(4, 8))):
+                per = st[:, ws, :5].sum(axis=(0, 1)) / taps[:, ws].sum()
+                print(f"  {grp:15s} " + "  ".join(f"{n}: {v:6.0f}" for n, v in zip(seg, per)) +
+                      f"  | total {per.sum():6.0f}", flush=True)
 
 
 if __name__ == "__main__":
