@@ -264,7 +264,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     }
   };
 
-  if constexpr (HALO == 2 || HALO == 4 || HALO == 5) {
+  if constexpr (HALO == 2 || HALO == 4) {
     // ---- ping-pong halo main loop (the default halo path; no GroupNorm-fused operand).  The two waves that
     //      share a SIMD (w and w + 4) take opposite roles in each half of a K step (slab c = kt / 9, tap
     //      t = kt % 9), so one of them always has MFMAs to issue while the other moves data:
@@ -288,12 +288,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     //      4 no B DMA, 8 no halo DMA, 16 no fragment reads, 32 no barriers; results are wrong when set).
     static_assert(S == 3 && KSUB == 2 && NW == 8 && CPR == 8 && RPI == 8, "ping-pong halo: 3-stage B ring, BK 64");
     constexpr bool DG = HALO == 4;
-    // HALO == 5 (option halo_pipe 3): the DMA pieces move out of the load phases into the compute phases, one piece
-    // after every run of 8 MFMAs (B(kt + 2) in group 1's compute phase of kt, slab c + 1's halo in group 0's compute
-    // phases of taps 0..5): a load phase is then only its fragment reads (+ group 1's wait for B(kt + 1)).  Ring
-    // safety: stage (kt - 1) % 3, which B(kt + 2) overwrites, was last read in the load phases of kt - 1, whose reads
-    // the same waves' MFMAs of kt - 1 consumed before this interval; the halo buffer of slab c - 1 likewise
-    constexpr bool CP = HALO == 5;
     const int dbg = DG ? a.dbg : 0;
     const int W = a.g.Win, H = a.g.Hin, lw = __builtin_ctz(W);
     const int HW = H * W;
@@ -342,11 +336,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       const uint32_t m = ldsB + (uint32_t)st * (BN * CPR * 16);
 #pragma unroll
       for (int j = 0; j < BPG; ++j) glds16_s(voffB, b + j * pstrB, m + j * 1024u);
-    };
-    auto issueB1 = [&](int c, auto tc, int st, int j) {   // piece j only
-      constexpr int t = decltype(tc)::value;
-      const char* b = bB + (long)(t * Cin + c * BK) * 2;
-      glds16_s(voffB, b + j * pstrB, ldsB + (uint32_t)st * (BN * CPR * 16) + j * 1024u);
     };
     // group 0: halo piece q = gw * HPG + j of slab c = pixels RPI * q .. + 7 of the (rows + 2) x W halo, which
     // starts at image pixel P0 = (img * H + y0 - 1) * W; a piece is wholly inside or outside the image
@@ -425,24 +414,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[ss][i], fb[ss][j], acc[i][j]);
     };
-    // the same 40 MFMAs in the same order, in 5 runs of 8, DMA piece k issued after run k (k < NP)
-    static_assert(KSUB * TM * TN == 40, "5 runs of 8 MFMAs");
-    auto mma_dma = [&](auto npc, auto&& piece) {
-      constexpr int NP = decltype(npc)::value;
-      static_for(std::make_integer_sequence<int, 5>{}, [&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        static_for(std::make_integer_sequence<int, 8>{}, [&](auto ec) {
-          constexpr int e = 8 * k + decltype(ec)::value;
-          constexpr int ss = e / (TM * TN), i = (e / TN) % TM, j = e % TN;
-          acc[i][j] = Mfma<T>::m16x16x32(fa[ss][i], fb[ss][j], acc[i][j]);
-        });
-        if constexpr (k < NP) {
-          __builtin_amdgcn_sched_barrier(0);
-          piece(kc);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      });
-    };
     // (sched_barrier: the MFMAs touch no memory, so without it the scheduler hoists them across the barrier asm
     // into the load phase, right behind the fragment reads they use — one wave then runs loads and MFMAs in
     // series and the two groups no longer alternate)
@@ -490,25 +461,15 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           IRX_STAMP(0);
           prio(true);
           readF(tc, Hs);
-          if constexpr (!CP) {
-            if constexpr (t < 7) issueB(c, std::integral_constant<int, t + 2>{}, (t + 2) % S);
-            else issueB(c + 1, std::integral_constant<int, t - 7>{}, (t + 2) % S);
-          }
+          if constexpr (t < 7) issueB(c, std::integral_constant<int, t + 2>{}, (t + 2) % S);
+          else issueB(c + 1, std::integral_constant<int, t - 7>{}, (t + 2) % S);
           IRX_STAMP(1);
-          wait_vm(CP ? 0 : BPG);
+          wait_vm(BPG);
           IRX_STAMP(2);
-          barrier(!CP && t == 8);
+          barrier(t == 8);
           IRX_STAMP(3);
           prio(false);
-          if constexpr (CP) {                            // compute phase (+ B(kt + 2))
-            mma_dma(std::integral_constant<int, BPG>{}, [&](auto kc) {
-              constexpr int k = decltype(kc)::value;
-              if constexpr (t < 7) issueB1(c, std::integral_constant<int, t + 2>{}, (t + 2) % S, k);
-              else issueB1(c + 1, std::integral_constant<int, t - 7>{}, (t + 2) % S, k);
-            });
-          } else {
-            mma();                                       // compute phase
-          }
+          mma();                                         // compute phase
           IRX_STAMP(4);
           barrier();
           IRX_STAMP(5);
@@ -527,7 +488,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           IRX_STAMP(0);
           prio(true);
           readF(tc, Hs);
-          if constexpr (t < HPARTS && !CP) {
+          if constexpr (t < HPARTS) {
             if (more) issueH(c + 1, t * HPP, (t + 1) * HPP);
           }
           IRX_STAMP(1);
@@ -535,14 +496,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           barrier(false);
           IRX_STAMP(3);
           prio(false);
-          if constexpr (CP && t < HPARTS) {              // compute phase (+ a sixth of slab c + 1's halo)
-            mma_dma(std::integral_constant<int, HPP>{}, [&](auto kc) {
-              constexpr int k = decltype(kc)::value;
-              if (more) issueH(c + 1, t * HPP + k, t * HPP + k + 1);
-            });
-          } else {
-            mma();                                       // compute phase
-          }
+          mma();                                         // compute phase
           if constexpr (t == 8) wait_vm(0);              // slab c + 1's halo landed
           IRX_STAMP(4);
           barrier();
@@ -1617,7 +1571,6 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
       sp.cnt = stream_counters(s);
     }
     if (g_halo_pipe && !a.gn_ab && b.dbg && a.dtype == BF16) launch2<256, 160, 4, 2, 64, 3, 4>(b, sp, s);   // (diagnostics)
-    else if (g_halo_pipe == 3 && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 5>(b, sp, s);   // DMA in compute phases
     else if (g_halo_pipe && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 2>(b, sp, s);   // ping-pong main loop
     else launch2<256, 160, 4, 2, 64, 3, 1>(b, sp, s);
     return true;

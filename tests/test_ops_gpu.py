@@ -486,12 +486,11 @@ def test_conv_halo_pipelined_bit_exact(device, case, dt):
     L.call("irx_set_option", b"conv_halo", 2 if forced else 1)
     try:
         outs = []
-        for pipe in (0, 1, 3):   # (3: the DMA pieces issued in the compute phases)
+        for pipe in (0, 1):
             L.call("irx_set_option", b"halo_pipe", pipe)
             outs.append(O.conv2d(x0, w.to(dt).float(), b, x1=x1, rowadd=temb, residual=res))
         torch.cuda.synchronize()
         assert torch.equal(outs[0], outs[1])
-        assert torch.equal(outs[0], outs[2])
     finally:
         L.call("irx_set_option", b"halo_pipe", 1)
         L.call("irx_set_option", b"conv_halo", 1)
