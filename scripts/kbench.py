@@ -78,11 +78,13 @@ def main():
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
     base = {"large_tiles": 1, "gemm_deep": 0, "gemm_small": 0, "tile_256x320": 1, "splitk_inkernel": 1, "halo_pipe": 1,
-            "gemm_pp": 0, "gemm_force": 0}
+            "gemm_pp": 0, "gemm_force": 0, "gemm_dbg": 0}
     allv = {"s2": {}, "ring64": {"gemm_deep": 2}, "ring32": {"gemm_deep": 1}, "small": {"gemm_small": 1}, "4wave": {"large_tiles": 0},
             "no320": {"tile_256x320": 0}, "redk": {"splitk_inkernel": 0}, "no320redk": {"tile_256x320": 0, "splitk_inkernel": 0},
             "halo1": {"halo_pipe": 0}, "halo2": {"halo_pipe": 1}, "pp0": {"gemm_pp": 0}, "pp1": {"gemm_pp": 1},
             "nm0": {"gemm_nmajor": 0},
+            # timing diagnostics (results wrong): 1 no epilogue, 2 no MFMAs, 3 neither
+            "dbg1": {"gemm_dbg": 1}, "dbg2": {"gemm_dbg": 2}, "dbg3": {"gemm_dbg": 3},
             # forced tile / split (gemm_force = BM*100000 + BN*100 + splits): the 8x8-level split-K sweep
             **{f"f{bm}x{bn}s{sp}": {"gemm_force": bm * 100000 + bn * 100 + sp}
                for bm in (256, 128) for bn in (320, 256, 128) for sp in (1, 2, 4, 8)}, "nm1": {"gemm_nmajor": 1}, "nm2": {"gemm_nmajor": 2}}
