@@ -843,6 +843,259 @@ __global__ __launch_bounds__(256, (PF ? PF : attn3_occ<D, KT>())) void attn3_ker
 }
 
 // ------------------------------------------------------------------------------------------------
+// attn3q: attn3 (non-causal, K/V streamed, whole-tile fragment prefetch) with TWO independent 32-query groups per
+// wave (block = 4 waves x 64 queries).  Every K fragment and V^T fragment read from LDS feeds both groups' MFMAs (half
+// the LDS reads per MFMA of attn3), and the two groups' softmax chains are independent, so one group's exp / convert
+// work can issue beside the other group's MFMAs inside one wave instead of relying on other waves for the overlap.
+// Per group the arithmetic is attn3's operation for operation (same MFMA order per accumulator, the deferred-max
+// decision taken over the group's own 32 queries), so the output is bit-identical.  2 waves / SIMD.
+template <typename T, int D, int KT>
+__global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
+  constexpr int G = 2;                                     // query groups per wave
+  constexpr int QB = 4 * 32 * G;                           // queries per block
+  constexpr int DQ = (D + 15) / 16 * 16, NS = DQ / 16;
+  constexpr int NDT = (D + 31) / 32;
+  constexpr bool ONES = D % 32 != 0;
+  constexpr int DVP = NDT * 32;
+  constexpr int SK = ((DQ / 8) % 2 == 0) ? DQ + 8 : DQ;
+  constexpr int SV = (DVP % 128 == 32 || DVP % 128 == 96) ? DVP : DVP + 32;
+  constexpr int NSUB = KT / 32;
+  constexpr int CPR = D / 8;
+  constexpr int NCH = (KT * CPR + 255) / 256;
+  constexpr float THR = 8.f;
+  constexpr bool PADM = DQ > D;
+  static_assert(D % 8 == 0 && KT % 32 == 0 && PADM && ONES, "attn3q: the d = 40 shape");
+  __shared__ __attribute__((aligned(16))) uint16_t Ks2[2 * KT * SK];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs2[2 * KT * SV];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5, g = lane >> 4;
+  const int nq = (a.Lq + QB - 1) / QB;
+  const int nblk = nq * a.H * a.B;
+  const int lid = a.xcd ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
+  const int qb = lid % nq, bh = lid / nq;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const T* __restrict__ Q = (const T*)a.q + (long)b * a.sq + (long)h * (a.hsq ? a.hsq : D);
+  const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : D);
+  const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : D);
+
+  for (int i = tid; i < 2 * KT * SK; i += 256) Ks2[i] = (i % SK == D) ? one_bits<T>() : (uint16_t)0;
+  for (int i = tid; i < 2 * KT * SV; i += 256) Vs2[i] = (i % SV == D) ? one_bits<T>() : (uint16_t)0;
+
+  uint4 kreg[NCH], vreg[NCH];
+  const T* kp[NCH];
+  const T* vp[NCH];
+  int krow[NCH], ksoff[NCH], vsoff[NCH];
+#pragma unroll
+  for (int u = 0; u < NCH; ++u) {
+    const int idx = min(tid + 256 * u, KT * CPR - 1);
+    const int row = idx / CPR, c = idx - row * CPR;
+    krow[u] = row;
+    kp[u] = K + (long)row * a.ldk + c * 8;
+    vp[u] = V + (long)row * a.ldv + c * 8;
+    ksoff[u] = row * SK + c * 8;
+    vsoff[u] = row * SV + c * 8;
+  }
+  auto slot_ok = [&](int u) { return u < NCH - 1 || tid + 256 * u < KT * CPR; };
+  auto load = [&](int j0) {
+    const long ko = (long)j0 * a.ldk, vo = (long)j0 * a.ldv;
+    if (j0 + KT <= a.Lk) {
+#pragma unroll
+      for (int u = 0; u < NCH; ++u)
+        if (slot_ok(u)) {
+          kreg[u] = *(const uint4*)(kp[u] + ko);
+          vreg[u] = *(const uint4*)(vp[u] + vo);
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const bool in = j0 + krow[u] < a.Lk;
+        kreg[u] = in ? *(const uint4*)(kp[u] + ko) : make_uint4(0, 0, 0, 0);
+        vreg[u] = in ? *(const uint4*)(vp[u] + vo) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u)
+      if (slot_ok(u)) {
+        *(uint4*)(Ks2 + buf * KT * SK + ksoff[u]) = kreg[u];
+        *(uint4*)(Vs2 + buf * KT * SV + vsoff[u]) = vreg[u];
+      }
+  };
+
+  const int q0 = qb * QB + wave * 32 * G;
+  uint4 qf[G][NS];
+  const float sl2 = a.scale * 1.4426950408889634f;
+#pragma unroll
+  for (int gq = 0; gq < G; ++gq)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int e = 16 * s + 8 * hh, qrow = q0 + 32 * gq + r;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (qrow < a.Lq && e < D) v = *(const uint4*)(Q + (long)qrow * a.ldq + e);
+      if (!a.q_scaled) {
+        float f[8];
+        Vec16<T>::unpack(v, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= sl2;
+        v = Vec16<T>::pack(f);
+      }
+      qf[gq][s] = v;
+    }
+  f32x16 oacc[G][NDT];
+#pragma unroll
+  for (int gq = 0; gq < G; ++gq)
+#pragma unroll
+    for (int i = 0; i < NDT; ++i)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) oacc[gq][i][k] = 0.f;
+  constexpr int PADS = D / 16;
+  float m[G] = {0.f, 0.f};
+  bool first = true;
+
+  const int kend = a.Lk;
+  load(0);
+  __syncthreads();
+  stage(0);
+  __syncthreads();
+  if (KT < kend) load(KT);
+
+  for (int j0 = 0, it = 0; j0 < kend; j0 += KT, ++it) {
+    const uint16_t* Ks = Ks2 + (it & 1) * KT * SK;
+    const uint16_t* Vs = Vs2 + (it & 1) * KT * SV;
+    f32x16 sacc[G][NSUB];
+#pragma unroll
+    for (int gq = 0; gq < G; ++gq)
+#pragma unroll
+      for (int c = 0; c < NSUB; ++c)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sacc[gq][c][k] = 0.f;
+    {
+      uint4 kf[NS][NSUB];
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int c = 0; c < NSUB; ++c) kf[s][c] = *(const uint4*)(Ks + (c * 32 + r) * SK + 16 * s + 8 * hh);
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int c = 0; c < NSUB; ++c)
+#pragma unroll
+          for (int gq = 0; gq < G; ++gq) sacc[gq][c] = Mfma<T>::m32x32x16(kf[s][c], qf[gq][s], sacc[gq][c]);
+    }
+    uint4 vpf[NSUB][NDT][2];
+#pragma unroll
+    for (int c = 0; c < NSUB; ++c)
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int krow = 32 * c + 16 * s2 + 4 * (g >> 1) + ((lane & 15) >> 2);
+          const int col = 32 * dt + 16 * (g & 1) + 4 * (lane & 3);
+          const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + krow * SV + col));
+          const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + (krow + 8) * SV + col));
+          vpf[c][dt][s2] = make_uint4(__builtin_bit_cast(uint2, t1).x, __builtin_bit_cast(uint2, t1).y,
+                                      __builtin_bit_cast(uint2, t2).x, __builtin_bit_cast(uint2, t2).y);
+        }
+    if (j0 + KT > a.Lk) {
+#pragma unroll
+      for (int gq = 0; gq < G; ++gq)
+#pragma unroll
+        for (int c = 0; c < NSUB; ++c)
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const int key = j0 + 32 * c + (k & 3) + 8 * (k >> 2) + 4 * hh;
+            if (key >= a.Lk) sacc[gq][c][k] = -INFINITY;
+          }
+    }
+    float tmax[G];
+#pragma unroll
+    for (int gq = 0; gq < G; ++gq) {
+      float mx[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) mx[t] = fmaxf(sacc[gq][0][4 * t], sacc[gq][0][4 * t + 1]);
+#pragma unroll
+      for (int c = 0; c < NSUB; ++c)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int k = (c == 0 ? 2 : 0); k < 4; k += 2)
+            mx[t] = fmaxf(fmaxf(mx[t], sacc[gq][c][4 * t + k]), sacc[gq][c][4 * t + k + 1]);
+      const float tm = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
+      tmax[gq] = fmaxf(tm, xlane32(tm));
+    }
+#pragma unroll
+    for (int gq = 0; gq < G; ++gq) {
+      if (first || __any(tmax[gq] > THR)) {
+        const float tgt = first ? (tmax[gq] == -INFINITY ? 0.f : m[gq] + tmax[gq]) : m[gq] + fmaxf(tmax[gq], 0.f);
+        const float mn = Mfma<T>::round(tgt);
+        const float delta = mn - m[gq];
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+#pragma unroll
+        for (int c = 0; c < NSUB; ++c)
+#pragma unroll
+          for (int k = 0; k < 16; ++k) sacc[gq][c][k] -= delta;
+        if (!first) {
+#pragma unroll
+          for (int i = 0; i < NDT; ++i)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) oacc[gq][i][k] *= alpha;
+        }
+        m[gq] = mn;
+        if (hh) qf[gq][PADS].x = (qf[gq][PADS].x & 0xFFFF0000u) | (Mfma<T>::pack2(-m[gq], 0.f) & 0xFFFFu);
+      }
+    }
+    first = false;
+#pragma unroll
+    for (int c = 0; c < NSUB; ++c) {
+      uint4 pb[G][2];
+#pragma unroll
+      for (int gq = 0; gq < G; ++gq)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          float p[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) p[j] = __builtin_amdgcn_exp2f(sacc[gq][c][8 * s2 + j]);
+          pb[gq][s2] = make_uint4(Mfma<T>::pack2(p[0], p[1]), Mfma<T>::pack2(p[2], p[3]), Mfma<T>::pack2(p[4], p[5]),
+                                  Mfma<T>::pack2(p[6], p[7]));
+        }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int gq = 0; gq < G; ++gq) oacc[gq][dt] = Mfma<T>::m32x32x16(vpf[c][dt][s2], pb[gq][s2], oacc[gq][dt]);
+    }
+    if (j0 + KT < kend) stage((it + 1) & 1);
+    __syncthreads();
+    if (j0 + 2 * KT < kend) load(j0 + 2 * KT);
+  }
+
+#pragma unroll
+  for (int gq = 0; gq < G; ++gq) {
+    constexpr int dts = D / 32, rho = D % 32, hs = (rho >> 2) & 1, reg = (rho & 3) + 4 * (rho >> 3);
+    const float v = oacc[gq][dts][reg];
+    const float o = xlane32(v);
+    const float l = hh == hs ? v : o;
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qrow = q0 + 32 * gq + r;
+    if (qrow < a.Lq) {
+      T* __restrict__ O = (T*)a.o + (long)b * a.so + (long)h * (a.hso ? a.hso : D) + (long)qrow * a.ldo;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int e = 32 * dt + 8 * k + 4 * hh;
+          if (e >= D) continue;
+          *(uint2*)(O + e) = make_uint2(Mfma<T>::pack2(oacc[gq][dt][4 * k] * inv, oacc[gq][dt][4 * k + 1] * inv),
+                                        Mfma<T>::pack2(oacc[gq][dt][4 * k + 2] * inv, oacc[gq][dt][4 * k + 3] * inv));
+        }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // attn3p: attn3 (non-causal, K/V streamed) with the QK^T MFMAs of key tile j+1 issued ahead of tile j's softmax, so
 // inside one wave the matrix pipe computes S(j+1) while the vector unit runs tile j's row max / exp / convert, then
 // tile j's PV MFMAs follow (software pipelining across key tiles; attn3 runs MFMA -> VALU -> MFMA serially per wave
@@ -1303,6 +1556,11 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
     }
   }
   if constexpr (!CAUSAL && D == 40) {
+    if (g_attn_q2) {   // two 32-query groups per wave (ProfScope above names attn3: the A/B is read from the timing)
+      attn3q_kernel<T, D, KT><<<dim3(((a.Lq + 255) / 256) * a.H * a.B), block, 0, s>>>(b);
+      IRX_LAUNCH_CHECK();
+      return;
+    }
     if (g_attn_pf) {   // (ProfScope above names attn3: the A/B is read from the timing, not the name)
       attn3_kernel<T, D, KT, false, false, 3><<<grid, block, 0, s>>>(b);
       IRX_LAUNCH_CHECK();
@@ -1401,6 +1659,7 @@ void attention(const AttnArgs& a, hipStream_t s) {
   else launch_t<bf16_t>(a, s);
 }
 int g_attn_v3 = 1;
+int g_attn_q2 = 0;     // irx_set_option("attn_q2", 1): d = 40 self-attention with two query groups per wave (attn3q, A/B)
 int g_attn_pf = 1;     // irx_set_option("attn_pf", 0): d = 40 self-attention without the whole-tile fragment prefetch (A/B)
 int g_attn_pipe = 0;   // irx_set_option("attn_pipe", 1): d = 40 self-attention on attn3p (QK^T one key tile ahead; A/B)
 int g_attn_xcd = 1;

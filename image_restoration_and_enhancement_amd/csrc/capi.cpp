@@ -76,6 +76,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gn_fold", &g_gn_fold, nullptr},
     {"attn_pipe", &g_attn_pipe, nullptr},
     {"attn_pf", &g_attn_pf, nullptr},
+    {"attn_q2", &g_attn_q2, nullptr},
     {"halo_split", &g_halo_split, nullptr},
     {"halo_pipe", &g_halo_pipe, nullptr},
     {"gemm_pp", &g_gemm_pp, nullptr},

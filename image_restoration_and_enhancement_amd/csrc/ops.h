@@ -212,6 +212,7 @@ struct AttnArgs {
 void attention(const AttnArgs& a, hipStream_t s);
 extern bool g_attn_v2;
 extern int g_attn_v3;    // 32x32x16 kernel for bf16 / fp16 (0: the round-1 kernels, bf16 only)
+extern int g_attn_q2;    // 1: non-causal streamed d = 40 attention with two 32-query groups per wave (attn3q)
 extern int g_attn_pf;    // 1: non-causal streamed d = 40 attention with whole-tile K / V fragment prefetch (attn3 PF)
 extern int g_attn_pipe;  // 1: non-causal streamed d = 40 attention with QK^T one key tile ahead (attn3p)
 extern int g_attn_prio;

@@ -140,16 +140,16 @@ def main():
             v = torch.randn(B, Lk, C, device=dev, generator=g).to(dt)
             flops = 4.0 * B * Lq * Lk * C
             res = []
-            for vn, v2 in (("v2", 1),):
-                L.call("irx_set_option", b"attn_v2", v2)
-                ms = timeit(lambda: O.attention(q, k, v, 8), args.iters)
+            for vn, opts in (("pf", {"attn_pf": 1, "attn_q2": 0}), ("nopf", {"attn_pf": 0, "attn_q2": 0}),
+                             ("q2", {"attn_pf": 1, "attn_q2": 1})):
+                with L.option(**opts):
+                    ms = timeit(lambda: O.attention(q, k, v, 8), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             if args.ref:   # torch SDPA (the ROCm flash / CK path) on the same data
                 hd = C // 8
                 qh, kh, vh = (t.view(B, -1, 8, hd).transpose(1, 2) for t in (q, k, v))
                 ms = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qh, kh, vh), args.iters)
                 res.append(f"sdpa {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
-            L.call("irx_set_option", b"attn_v2", 1)
             print(f"{lab:24s} " + " | ".join(res), flush=True)
 
 

@@ -740,3 +740,21 @@ def test_attention_prefetch_d40_bit_exact(device, dt, B, Lq, Lk):
         base = O.attention(qd, kd, vd, heads)
     torch.cuda.synchronize()
     assert torch.equal(got, base)
+
+
+@pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("B,Lq,Lk", [(2, 1024, 1024), (1, 333, 190), (1, 64, 129), (2, 4096, 4096)])
+def test_attention_two_query_groups_d40_bit_exact(device, dt, B, Lq, Lk):
+    """attn3q (option attn_q2: two 32-query groups per wave sharing every K / V^T fragment read) runs each group's
+    arithmetic exactly as attn3 does (same MFMA order per accumulator, the deferred-max decision over the group's own
+    queries): identical outputs bit for bit, ragged query and key counts included."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    C, heads = 320, 8
+    q, k, v = _r(B, Lq, C, seed=76) * 2, _r(B, Lk, C, seed=77) * 2, _r(B, Lk, C, seed=78)
+    qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
+    with L.option(attn_q2=1):
+        got = O.attention(qd, kd, vd, heads)
+    with L.option(attn_q2=0):
+        base = O.attention(qd, kd, vd, heads)
+    torch.cuda.synchronize()
+    assert torch.equal(got, base)
