@@ -528,6 +528,10 @@ __global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
 template <typename T> constexpr uint16_t one_bits();
 template <> constexpr uint16_t one_bits<bf16_t>() { return 0x3F80; }
 template <> constexpr uint16_t one_bits<f16_t>() { return 0x3C00; }
+// a large negative score offset of the storage type (-65536 in bf16, -65504 in fp16): exp2 of it is exactly 0 in fp32
+template <typename T> constexpr uint16_t neg_big_bits();
+template <> constexpr uint16_t neg_big_bits<bf16_t>() { return 0xC780; }
+template <> constexpr uint16_t neg_big_bits<f16_t>() { return 0xFBFF; }
 
 __device__ __forceinline__ float xlane32(float x) {   // value of lane l ^ 32
   const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -879,6 +883,8 @@ __global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
   const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : D);
   const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : D);
 
+  // K pad columns: d = 1 (carries -m from Q), d + 1 = the key mask (0; neg_big for keys past Lk, Q[d + 1] = 1), so
+  // a ragged last key tile needs no compare / select pass over the scores
   for (int i = tid; i < 2 * KT * SK; i += 256) Ks2[i] = (i % SK == D) ? one_bits<T>() : (uint16_t)0;
   for (int i = tid; i < 2 * KT * SV; i += 256) Vs2[i] = (i % SV == D) ? one_bits<T>() : (uint16_t)0;
 
@@ -915,13 +921,15 @@ __global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
       }
     }
   };
-  auto stage = [&](int buf) {
+  auto stage = [&](int buf, int j0) {
 #pragma unroll
     for (int u = 0; u < NCH; ++u)
       if (slot_ok(u)) {
         *(uint4*)(Ks2 + buf * KT * SK + ksoff[u]) = kreg[u];
         *(uint4*)(Vs2 + buf * KT * SV + vsoff[u]) = vreg[u];
       }
+    if (j0 + KT > a.Lk && tid < KT && j0 + tid >= a.Lk)   // (the last tile is the only partial one)
+      Ks2[buf * KT * SK + tid * SK + D + 1] = neg_big_bits<T>();
   };
 
   const int q0 = qb * QB + wave * 32 * G;
@@ -941,6 +949,7 @@ __global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
         for (int j = 0; j < 8; ++j) f[j] *= sl2;
         v = Vec16<T>::pack(f);
       }
+      if (e == D) v.x = (uint32_t)one_bits<T>() << 16;   // Q[d + 1] = 1: the key-mask column
       qf[gq][s] = v;
     }
   f32x16 oacc[G][NDT];
@@ -957,7 +966,7 @@ __global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
   const int kend = a.Lk;
   load(0);
   __syncthreads();
-  stage(0);
+  stage(0, 0);
   __syncthreads();
   if (KT < kend) load(KT);
 
@@ -977,12 +986,13 @@ __global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
       for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int c = 0; c < NSUB; ++c) kf[s][c] = *(const uint4*)(Ks + (c * 32 + r) * SK + 16 * s + 8 * hh);
+      // (group-major: group 0's scores complete while group 1's MFMAs still run, so its row max can start)
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
+      for (int gq = 0; gq < G; ++gq)
 #pragma unroll
-        for (int c = 0; c < NSUB; ++c)
+        for (int s = 0; s < NS; ++s)
 #pragma unroll
-          for (int gq = 0; gq < G; ++gq) sacc[gq][c] = Mfma<T>::m32x32x16(kf[s][c], qf[gq][s], sacc[gq][c]);
+          for (int c = 0; c < NSUB; ++c) sacc[gq][c] = Mfma<T>::m32x32x16(kf[s][c], qf[gq][s], sacc[gq][c]);
     }
     uint4 vpf[NSUB][NDT][2];
 #pragma unroll
@@ -998,17 +1008,6 @@ __global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
           vpf[c][dt][s2] = make_uint4(__builtin_bit_cast(uint2, t1).x, __builtin_bit_cast(uint2, t1).y,
                                       __builtin_bit_cast(uint2, t2).x, __builtin_bit_cast(uint2, t2).y);
         }
-    if (j0 + KT > a.Lk) {
-#pragma unroll
-      for (int gq = 0; gq < G; ++gq)
-#pragma unroll
-        for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-          for (int k = 0; k < 16; ++k) {
-            const int key = j0 + 32 * c + (k & 3) + 8 * (k >> 2) + 4 * hh;
-            if (key >= a.Lk) sacc[gq][c][k] = -INFINITY;
-          }
-    }
     float tmax[G];
 #pragma unroll
     for (int gq = 0; gq < G; ++gq) {
@@ -1067,7 +1066,7 @@ __global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
 #pragma unroll
           for (int gq = 0; gq < G; ++gq) oacc[gq][dt] = Mfma<T>::m32x32x16(vpf[c][dt][s2], pb[gq][s2], oacc[gq][dt]);
     }
-    if (j0 + KT < kend) stage((it + 1) & 1);
+    if (j0 + KT < kend) stage((it + 1) & 1, j0 + KT);
     __syncthreads();
     if (j0 + 2 * KT < kend) load(j0 + 2 * KT);
   }
@@ -1659,7 +1658,7 @@ void attention(const AttnArgs& a, hipStream_t s) {
   else launch_t<bf16_t>(a, s);
 }
 int g_attn_v3 = 1;
-int g_attn_q2 = 0;     // irx_set_option("attn_q2", 1): d = 40 self-attention with two query groups per wave (attn3q, A/B)
+int g_attn_q2 = 1;     // irx_set_option("attn_q2", 0): d = 40 self-attention with one query group per wave (attn3, A/B)
 int g_attn_pf = 1;     // irx_set_option("attn_pf", 0): d = 40 self-attention without the whole-tile fragment prefetch (A/B)
 int g_attn_pipe = 0;   // irx_set_option("attn_pipe", 1): d = 40 self-attention on attn3p (QK^T one key tile ahead; A/B)
 int g_attn_xcd = 1;

@@ -734,9 +734,9 @@ def test_attention_prefetch_d40_bit_exact(device, dt, B, Lq, Lk):
     C, heads = 320, 8
     q, k, v = _r(B, Lq, C, seed=73) * 2, _r(B, Lk, C, seed=74) * 2, _r(B, Lk, C, seed=75)
     qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
-    with L.option(attn_pf=1):
+    with L.option(attn_pf=1, attn_q2=0):
         got = O.attention(qd, kd, vd, heads)
-    with L.option(attn_pf=0):
+    with L.option(attn_pf=0, attn_q2=0):
         base = O.attention(qd, kd, vd, heads)
     torch.cuda.synchronize()
     assert torch.equal(got, base)
@@ -754,7 +754,7 @@ def test_attention_two_query_groups_d40_bit_exact(device, dt, B, Lq, Lk):
     qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
     with L.option(attn_q2=1):
         got = O.attention(qd, kd, vd, heads)
-    with L.option(attn_q2=0):
+    with L.option(attn_q2=0, attn_pf=0):
         base = O.attention(qd, kd, vd, heads)
     torch.cuda.synchronize()
     assert torch.equal(got, base)
