@@ -662,6 +662,101 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  } else if constexpr (PP && !CONV) {
+    // ---- lean ping-pong for dense GEMMs (host: whole tiles, M % BM == N % BN == 0): the halo loop's form.  The
+    //      waves w and w + 4 sharing a SIMD alternate a load phase (this wave's fragment reads of step kt, then its
+    //      LDS-DMA pieces of step kt + 2) and a compute phase (step kt's MFMAs), group 1 one phase behind group 0.
+    //      Every piece is one SADDR-form DMA: a wave-uniform row base in SGPRs + a per-lane byte offset fixed for
+    //      the kernel; the step's K offset is a scalar add; the two steps past the split's end re-issue its last
+    //      step into the free stage, so every wait count is a constant.  The stage index is compile-time (the K loop
+    //      unrolled by 3) and the phases are pinned by sched_barrier (else the MFMAs, which touch no memory, move
+    //      into the load phase).  Group 1's load barrier drains its reads: group 0's next DMA targets the stage they
+    //      read; group 0's does not (each MFMA waits for its own operands).
+    static_assert(S == 3 && NW == 8, "ping-pong: 3 stages, 8 waves");
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const bool g1 = wv >= NW / 2;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)smem);
+    const char* pb[IPW];
+    uint32_t pv[IPW], pd[IPW];
+#pragma unroll
+    for (int j = 0; j < IPW; ++j) {
+      const int q = wv * IPW + j, r0 = RPI * q, r = r0 + lrow;
+      const int ch = (lslot ^ swz(r)) * 8;
+      if (q < NINST && r0 < BM) {
+        pb[j] = (const char*)(Ap + (long)(m0 + r0) * a.lda);
+        pv[j] = (uint32_t)(lrow * a.lda + ch) * 2u;
+      } else if (q < NINST) {
+        pb[j] = (const char*)(Bp + (long)(n0 + r0 - BM) * a.ldb);
+        pv[j] = (uint32_t)(lrow * a.ldb + ch) * 2u;
+      } else {   // surplus piece: any in-range source, into the scratch KiB
+        pb[j] = (const char*)(Ap + (long)m0 * a.lda);
+        pv[j] = (uint32_t)lane * 16u;
+      }
+      pd[j] = q < NINST ? lds0 + (uint32_t)(q * 64) * 16u : lds0 + (uint32_t)(SMEM - 64) * 16u;
+    }
+    auto issueP = [&](int kt, int st) {
+      const long ko = (long)kt * BK * 2;
+      const uint32_t so = (uint32_t)(st * STAGE) * 16u;
+#pragma unroll
+      for (int j = 0; j < IPW; ++j)
+        glds16_s(pv[j], pb[j] + ko, wv * IPW + j < NINST ? pd[j] + so : pd[j]);
+    };
+    uint4 fa[KSUB][TM], fb[KSUB][TN];
+    auto readF = [&](auto stc) {
+      constexpr int st = decltype(stc)::value;
+      const uint4* As = smem + st * STAGE;
+      const uint4* Bs = As + BM * CPR;
+#pragma unroll
+      for (int s = 0; s < KSUB; ++s) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * TM * 16 + i * 16 + frow;
+          fa[s][i] = As[r * CPR + ((s * 4 + fgrp) ^ swz(r))];
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * TN * 16 + j * 16 + frow;
+          fb[s][j] = Bs[r * CPR + ((s * 4 + fgrp) ^ swz(r + BM))];
+        }
+      }
+    };
+    auto mma = [&]() {
+#pragma unroll
+      for (int s = 0; s < KSUB; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = Mfma<T>::m16x16x32(fa[s][i], fb[s][j], acc[i][j]);
+    };
+    auto barrier = [&](bool drain) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (drain) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    issueP(kt0, 0);
+    issueP(min(kt0 + 1, kt1 - 1), 1);
+    wait_vm(IPW);                                        // step kt0 landed
+    barrier(true);
+    if (g1) barrier(true);
+    for (int kb = kt0; kb < kt1; kb += 3) {
+      static_for(std::make_integer_sequence<int, 3>{}, [&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        const int kt = kb + u;
+        if (kt < kt1) {
+          readF(uc);                                     // load phase
+          issueP(min(kt + 2, kt1 - 1), (u + 2) % 3);
+          if (g1) wait_vm(IPW);                          // step kt + 1 landed (group 0 reads it next)
+          barrier(g1);
+          mma();                                         // compute phase
+          if (!g1) wait_vm(IPW);
+          barrier(true);
+        }
+      });
+    }
+    if (!g1) barrier(true);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   } else if constexpr (PP) {
     // ---- ping-pong main loop (the dense GEMM / im2col conv counterpart of the HALO == 2 schedule): the waves
     //      w and w + 4 sharing a SIMD alternate between a load phase (LDS-DMA of step kt + 2, this wave's
@@ -1609,7 +1704,8 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   if (c.small) {
     if (c.BN == 160) launch2<128, 160, 2, 2, 64, 2>(b, sp, s);
     else launch2<128, 128, 2, 2, 64, 2>(b, sp, s);
-  } else if (g_gemm_pp && g_gemm_deep == 0) {   // ping-pong schedule: 3 stages (BK 32 where BK 64 would not fit)
+  } else if (g_gemm_pp && g_gemm_deep == 0 && (a.conv || (a.M % c.BM == 0 && a.N % c.BN == 0))) {
+    // ping-pong schedule: 3 stages (BK 32 where BK 64 would not fit); dense GEMMs on whole tiles only (the lean form)
     const int key = c.BM * 1000 + c.BN;
     if (key == 256320 || key == 256256 || key == 128320) sp.per *= 2;   // K steps of 32
     switch (key) {
