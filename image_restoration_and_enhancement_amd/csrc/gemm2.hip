@@ -1560,7 +1560,7 @@ bool gemm_emits_ln_parts(const GemmArgs& a) {
     const long tiles = (long)((a.M + c.BM - 1) / c.BM) * ((a.N + c.BN - 1) / c.BN);
     if (!(g_splitk_inkernel && c.splits == 2 && tiles <= kSplitCounters)) return false;
   }
-  return !g_gemm_pp && g_gemm_deep == 0;
+  return g_gemm_pp != 1 && g_gemm_deep == 0;
 }
 
 int g_gn_fold = 1;
@@ -1575,7 +1575,7 @@ bool gemm_bimg_ok(const GemmArgs& a) {
     const long tiles = (long)((a.M + c.BM - 1) / c.BM) * ((a.N + c.BN - 1) / c.BN);
     if (!(g_splitk_inkernel && c.splits == 2 && tiles <= kSplitCounters)) return false;
   }
-  return !g_gemm_pp && g_gemm_deep == 0;
+  return g_gemm_pp != 1 && g_gemm_deep == 0;
 }
 
 bool gemm_geglu_fusable(const GemmArgs& a) {
@@ -1607,10 +1607,11 @@ size_t gemm_workspace_bytes(const GemmArgs& a) {
 // reduction) when two splits do, 0 = the halo path does not take the shape.
 int g_halo_split = 1;   // irx_set_option("halo_split", 0): no K-split halo tiles (A/B)
 int g_halo_pipe = 1;    // irx_set_option("halo_pipe", 0): the round-2 halo main loop (A/B)
-// irx_set_option("gemm_pp", 1): ping-pong main loop for dense GEMMs / im2col convs.  Off: measured slower at every
-// UNet / VAE shape (bench 553.8 vs 515.7 ms/step, the VAE 512x512 convs 1.9x; profiles/r03_kbench_*_pp.txt) — the
-// halo conv's gain came with its unrolled-tap addressing, which these loops do not need
-int g_gemm_pp = 0;
+// irx_set_option("gemm_pp", m): ping-pong main loops.  2 (default): the lean dense form on 256x256 tiles only (the
+// 32x32 / 16x16-level GEGLU projections: ff1 -12 / -14 % at the kbench shapes, 49.9 -> 46.5 ms/step in the bench;
+// profiles/r04_kbench_gemm_pp_lean.txt); 1: every dense / im2col tile (the im2col convs keep the round-3 branchy form,
+// which is slower there, and the lean form loses at 128x128 / 1280-wide 16x16 shapes); 0: none
+int g_gemm_pp = 2;
 
 int halo_splits(const GemmArgs& a, long tiles) {
   if (tiles >= kCUs || g_conv_halo >= 2) return 1;
@@ -1704,7 +1705,8 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   if (c.small) {
     if (c.BN == 160) launch2<128, 160, 2, 2, 64, 2>(b, sp, s);
     else launch2<128, 128, 2, 2, 64, 2>(b, sp, s);
-  } else if (g_gemm_pp && g_gemm_deep == 0 && (a.conv || (a.M % c.BM == 0 && a.N % c.BN == 0))) {
+  } else if (g_gemm_deep == 0 && (g_gemm_pp == 1 || (g_gemm_pp == 2 && c.BM == 256 && c.BN == 256 && !a.ln_out && !a.b_rows)) &&
+             (a.conv || (a.M % c.BM == 0 && a.N % c.BN == 0)) && !(g_gemm_pp == 2 && a.conv)) {
     // ping-pong schedule: 3 stages (BK 32 where BK 64 would not fit); dense GEMMs on whole tiles only (the lean form)
     const int key = c.BM * 1000 + c.BN;
     if (key == 256320 || key == 256256 || key == 128320) sp.per *= 2;   // K steps of 32

@@ -81,7 +81,7 @@ def main():
             "gemm_pp": 0, "gemm_force": 0, "gemm_dbg": 0}
     allv = {"s2": {}, "ring64": {"gemm_deep": 2}, "ring32": {"gemm_deep": 1}, "small": {"gemm_small": 1}, "4wave": {"large_tiles": 0},
             "no320": {"tile_256x320": 0}, "redk": {"splitk_inkernel": 0}, "no320redk": {"tile_256x320": 0, "splitk_inkernel": 0},
-            "halo1": {"halo_pipe": 0}, "halo2": {"halo_pipe": 1}, "pp0": {"gemm_pp": 0}, "pp1": {"gemm_pp": 1},
+            "halo1": {"halo_pipe": 0}, "halo2": {"halo_pipe": 1}, "pp0": {"gemm_pp": 0}, "pp1": {"gemm_pp": 1}, "pp2": {"gemm_pp": 2},
             "nm0": {"gemm_nmajor": 0},
             # timing diagnostics (results wrong): 1 no epilogue, 2 no MFMAs, 3 neither
             "dbg1": {"gemm_dbg": 1}, "dbg2": {"gemm_dbg": 2}, "dbg3": {"gemm_dbg": 3},

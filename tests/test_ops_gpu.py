@@ -502,18 +502,21 @@ def test_conv_halo_pipelined_bit_exact(device, case, dt):
     (4096, 1280, 1280, False, None),      # 16x16 level (128x128 tiles, BK 64, split-K)
     (1000, 256, 512, False, None),        # ragged M
     (65536, 1280, 320, False, "geglu"),   # GEGLU epilogue (256x256, BK 32)
+    (16384, 5120, 640, False, None),      # 32x32-level FF projection shape (256x256 tiles)
+    (4096, 2560, 1280, False, "geglu"),   # 16x16-level GEGLU (256x256, K = 1280)
     (0, 640, 0, False, (16, 16, 16, 1280, 640)),   # im2col conv: 16x16 level, 1280 -> 640
     (0, 320, 0, False, (8, 32, 32, 640, 320)),     # im2col conv: upsample-free 32x32, 640 -> 320 (1x1 shortcut)
 ])
 @pytest.mark.parametrize("dt", DT16)
 def test_gemm_pingpong_bit_exact(device, M, N, K, res, conv, dt):
-    """The ping-pong main loop (option gemm_pp; off by default, measured slower) issues every accumulator's MFMAs in the round-2 order
-    (32-deep K sub-steps, ascending; the same split-K boundaries): outputs identical bit for bit."""
+    """The ping-pong main loops (option gemm_pp: 2 = the lean dense form on 256x256 tiles, the default; 1 = every tile)
+    issue every accumulator's MFMAs in the round-2 order (32-deep K sub-steps, ascending; the same split-K
+    boundaries): outputs identical bit for bit to the two-stage loop (0)."""
     from image_restoration_and_enhancement_amd import _lib as L
     from image_restoration_and_enhancement_amd.engine import geglu64_order
     outs = []
     try:
-        for pp in (0, 1):
+        for pp in (0, 1, 2):
             L.call("irx_set_option", b"gemm_pp", pp)
             if conv == "geglu":
                 C = K
@@ -537,8 +540,9 @@ def test_gemm_pingpong_bit_exact(device, M, N, K, res, conv, dt):
                 outs.append(O.gemm(A, Bw, bias=_r(N, seed=309).to(device).contiguous(), residual=r))
         torch.cuda.synchronize()
         assert torch.equal(outs[0], outs[1])
+        assert torch.equal(outs[0], outs[2])
     finally:
-        L.call("irx_set_option", b"gemm_pp", 0)
+        L.call("irx_set_option", b"gemm_pp", 2)
 
 
 @pytest.mark.parametrize("B,L", [(2, 256), (1, 333), (2, 1024), (1, 77)])
