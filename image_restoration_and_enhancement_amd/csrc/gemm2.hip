@@ -1705,8 +1705,10 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   if (c.small) {
     if (c.BN == 160) launch2<128, 160, 2, 2, 64, 2>(b, sp, s);
     else launch2<128, 128, 2, 2, 64, 2>(b, sp, s);
-  } else if (g_gemm_deep == 0 && (g_gemm_pp == 1 || (g_gemm_pp == 2 && c.BM == 256 && c.BN == 256 && !a.ln_out && !a.b_rows)) &&
-             (a.conv || (a.M % c.BM == 0 && a.N % c.BN == 0)) && !(g_gemm_pp == 2 && a.conv)) {
+  } else if (g_gemm_deep == 0 &&
+             (g_gemm_pp == 1 || (g_gemm_pp >= 2 && !a.conv && c.BM == 256 && (c.BN == 256 || (g_gemm_pp == 3 && c.BN == 320)) &&
+                                 !a.ln_out && !a.b_rows)) &&
+             (a.conv || (a.M % c.BM == 0 && a.N % c.BN == 0))) {
     // ping-pong schedule: 3 stages (BK 32 where BK 64 would not fit); dense GEMMs on whole tiles only (the lean form)
     const int key = c.BM * 1000 + c.BN;
     if (key == 256320 || key == 256256 || key == 128320) sp.per *= 2;   // K steps of 32
