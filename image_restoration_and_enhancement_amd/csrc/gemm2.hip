@@ -1610,7 +1610,8 @@ int g_halo_pipe = 1;    // irx_set_option("halo_pipe", 0): the round-2 halo main
 // irx_set_option("gemm_pp", m): ping-pong main loops.  2 (default): the lean dense form on 256x256 tiles only (the
 // 32x32 / 16x16-level GEGLU projections: ff1 -12 / -14 % at the kbench shapes, 49.9 -> 46.5 ms/step in the bench;
 // profiles/r04_kbench_gemm_pp_lean.txt); 1: every dense / im2col tile (the im2col convs keep the round-3 branchy form,
-// which is slower there, and the lean form loses at 128x128 / 1280-wide 16x16 shapes); 0: none
+// which is slower there, and the lean form loses at 128x128 / 1280-wide 16x16 shapes); 3: 256x256 + 256x320 (measured
+// 513.7 vs 508.2 ms/step: off); 0: none
 int g_gemm_pp = 2;
 
 int halo_splits(const GemmArgs& a, long tiles) {
