@@ -37,7 +37,7 @@ PASSES = {
     "fetch": "FETCH_SIZE",
     "write": "WRITE_SIZE",
 }
-KERNELS = "gemm2_kernel|gemm_sk_kernel|attn3_kernel|attnw_kernel|gemm_kernel|attn_kernel"   # (adding gn_apply / ln_kernel made the FETCH pass crash inside the profiler, round 3)
+KERNELS = "gemm2_kernel|gemm_sk_kernel|attn3_kernel|attn3q_kernel|attnw_kernel|gemm_kernel|attn_kernel"   # (adding gn_apply / ln_kernel made the FETCH pass crash inside the profiler, round 3)
 SIMDS = 1024
 XCDS = 8
 
