@@ -25,11 +25,16 @@ Also reported (rank 0):
                  reference's own diffusers path cannot run here) on configs[0]: full 512x512 denoise
                  images, 20 PNDM steps x strength 0.5 (11 UNet evals, CFG), on this process's usable
                  host cores (N = 1 only);
-  parity       — the same configs[0] image through the GPU engine (fp32 and bf16): max |decoded pixel
-                 difference| of the fp32 engine vs the CPU reference, PSNR/SSIM (metrics.py, pinned to
-                 scikit-image) of the bf16 output vs the CPU reference output, of all three outputs vs the
-                 clean ground truth, and whether each engine's mean PSNR / SSIM equal the CPU reference's to
-                 3 significant figures (the north star's "PSNR/SSIM reproduced to 3 s.f.").
+  parity       — the same configs[0] images through the GPU engines (fp32; the bench's bf16 UNet + CLIP with
+                 the fp16 VAE; all-bf16; all-fp16, the reference's GPU dtype): max |decoded pixel difference| of
+                 the fp32 engine vs the CPU reference, PSNR/SSIM (metrics.py, pinned to scikit-image) of the
+                 bench engine's output vs the CPU reference output, of every output vs the clean ground truth
+                 (per image and as means), and whether each engine's mean PSNR / SSIM equal the CPU reference's
+                 to 3 significant figures (the north star's "PSNR/SSIM reproduced to 3 s.f.").
+
+Compute types: the bf16 tasks run the UNet and CLIP in bf16 and the VAE in fp16 (same MFMA rate): the bf16 VAE
+is the stage whose rounding moves the configs[0] SSIM at the third figure (profiles/r05_parity_stages.txt,
+DESIGN.md §5); `--vae-dtype bf16` gives the all-bf16 engine.
 """
 from __future__ import annotations
 
@@ -66,10 +71,10 @@ PROMPTS = {   # src/inference.py:86-91
 }
 # BASELINE.json configs[1..4] as per-GPU workloads
 TASKS = {
-    "denoise": dict(cfg=2, res=512, batch=8, strength=0.5, guidance=5.0, dtype="bf16", n_enc=1),
-    "sr": dict(cfg=3, res=512, lr=128, batch=16, strength=0.8, guidance=0.0, dtype="bf16", n_enc=1),
-    "inpaint": dict(cfg=4, res=512, batch=8, strength=0.6, guidance=5.0, dtype="bf16", n_enc=2),
-    "colorize": dict(cfg=5, res=768, batch=8, strength=0.75, guidance=7.5, dtype="fp16", n_enc=1),
+    "denoise": dict(cfg=2, res=512, batch=8, strength=0.5, guidance=5.0, dtype="bf16", vae="fp16", n_enc=1),
+    "sr": dict(cfg=3, res=512, lr=128, batch=16, strength=0.8, guidance=0.0, dtype="bf16", vae="fp16", n_enc=1),
+    "inpaint": dict(cfg=4, res=512, batch=8, strength=0.6, guidance=5.0, dtype="bf16", vae="fp16", n_enc=2),
+    "colorize": dict(cfg=5, res=768, batch=8, strength=0.75, guidance=7.5, dtype="fp16", vae="fp16", n_enc=1),
 }
 
 
@@ -127,8 +132,8 @@ def task_inputs(task: str, spec: dict, batch: int, seed: int):
     return noisy, None
 
 
-def build_engine(cfg, dtype, device, rank):
-    eng = SDEngine(cfg, dtype, device, weights="none")
+def build_engine(cfg, dtype, device, rank, vae_dtype=None):
+    eng = SDEngine(cfg, dtype, device, weights="none", vae_dtype=vae_dtype)
     models = eng.models()
     sds = None
     if rank == 0:
@@ -194,9 +199,9 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline_and_parity(eng_bf16, sds, device, n_images: int, threads: int) -> tuple:
+def cpu_baseline_and_parity(eng_bench, sds, device, n_images: int, threads: int) -> tuple:
     """configs[0] on the host cores through the fp32 CPU restatement, plus the same images
-    through the GPU engine (fp32 and bf16) for the parity report."""
+    through the GPU engines for the parity report."""
     from image_restoration_and_enhancement_amd import metrics as M
     from oracle import pipeline_ref as PR
     from image_restoration_and_enhancement_amd.tokenizer import PromptTokenizer
@@ -226,29 +231,36 @@ def cpu_baseline_and_parity(eng_bf16, sds, device, n_images: int, threads: int) 
                      f"process ({threads}); {per_img:.1f} s/image, model load excluded",
            "seconds_per_image": [round(t, 2) for t in t_img]}
 
-    # the same images through the GPU engine
+    # the same images through the GPU engines: fp32, the bench engine, all-bf16, all-fp16 (the reference's GPU dtype)
     u8 = torch.from_numpy(noisy).to(device).contiguous()
-    eng32 = SDEngine(cfg, "fp32", device, state_dicts=sds)
-    g32 = eng32.img2img(u8, prompt, strength, steps, guidance, seed=42, want_float=True)
-    del eng32
-    kind = eng_bf16.cfg.scheduler.kind
-    eng_bf16.cfg.scheduler.kind = "pndm"
-    try:
-        g16 = eng_bf16.img2img(u8, prompt, strength, steps, guidance, seed=42, want_float=True)
-    finally:
-        eng_bf16.cfg.scheduler.kind = kind
+    bench_key = "gpu_bf16_vae_fp16"
+
+    def run(eng):
+        kind = eng.cfg.scheduler.kind
+        eng.cfg.scheduler.kind = "pndm"
+        try:
+            return eng.img2img(u8, prompt, strength, steps, guidance, seed=42, want_float=True)
+        finally:
+            eng.cfg.scheduler.kind = kind
+
+    outs = {}
+    for key, dt, vdt in (("gpu_fp32", "fp32", None), ("gpu_bf16", "bf16", "bf16"), ("gpu_fp16", "fp16", "fp16")):
+        e = SDEngine(cfg, dt, device, state_dicts=sds, vae_dtype=vdt)
+        outs[key] = run(e)
+        del e
+    outs[bench_key] = run(eng_bench)
     torch.cuda.synchronize()
     f32_max, u8_max, ps, ss = 0.0, 0, [], []
-    gt = {k: ([], []) for k in ("gpu_fp32", "gpu_bf16", "cpu_ref")}   # (PSNR, SSIM) vs the clean image, per image
+    keys = ("gpu_fp32", bench_key, "gpu_bf16", "gpu_fp16")
+    gt = {k: ([], []) for k in keys + ("cpu_ref",)}   # (PSNR, SSIM) vs the clean image, per image
     for i, r in enumerate(refs):
         ref_u8 = np.asarray(r.image)
-        f32_max = max(f32_max, float(np.abs(g32.decoded01[i].cpu().numpy() - r.decoded_float).max()))
-        a = g32.images_u8[i].cpu().numpy()
-        u8_max = max(u8_max, int(np.abs(a.astype(int) - ref_u8.astype(int)).max()))
-        b = g16.images_u8[i].cpu().numpy()
-        ps.append(M.psnr(ref_u8, b))
-        ss.append(M.ssim(ref_u8, b))
-        for k, img in (("gpu_fp32", a), ("gpu_bf16", b), ("cpu_ref", ref_u8)):
+        f32_max = max(f32_max, float(np.abs(outs["gpu_fp32"].decoded01[i].cpu().numpy() - r.decoded_float).max()))
+        imgs = {k: outs[k].images_u8[i].cpu().numpy() for k in keys}
+        u8_max = max(u8_max, int(np.abs(imgs["gpu_fp32"].astype(int) - ref_u8.astype(int)).max()))
+        ps.append(M.psnr(ref_u8, imgs[bench_key]))
+        ss.append(M.ssim(ref_u8, imgs[bench_key]))
+        for k, img in list(imgs.items()) + [("cpu_ref", ref_u8)]:
             gt[k][0].append(M.psnr(clean[i], img))
             gt[k][1].append(M.ssim(clean[i], img))
     mean_gt = {k: (float(np.mean(v[0])), float(np.mean(v[1]))) for k, v in gt.items()}
@@ -258,21 +270,27 @@ def cpu_baseline_and_parity(eng_bf16, sds, device, n_images: int, threads: int) 
     # north star: "PSNR/SSIM reproduced to 3 s.f." — the task means (src/metrics.py:82-95 semantics: per-image PSNR /
     # SSIM against the clean image, averaged) of each GPU engine against the CPU reference's, both at 3 s.f.
     match = {k: sf3(mean_gt[k][0]) == sf3(mean_gt["cpu_ref"][0]) and sf3(mean_gt[k][1]) == sf3(mean_gt["cpu_ref"][1])
-             for k in ("gpu_fp32", "gpu_bf16")}
+             for k in keys}
+    per_img_d = {k: {"abs_d_psnr": [round(abs(a - b), 5) for a, b in zip(gt[k][0], gt["cpu_ref"][0])],
+                     "abs_d_ssim": [round(abs(a - b), 7) for a, b in zip(gt[k][1], gt["cpu_ref"][1])]}
+                 for k in keys}
     parity = {"workload": "BASELINE configs[0] images (512x512, 20 PNDM steps x 0.5, CFG 5.0, seed 42)",
-              "images": n_images,
+              "images": n_images, "bench_engine": bench_key,
               "fp32_engine_max_abs_vs_ref": f32_max, "fp32_engine_u8_max_diff_vs_ref": u8_max,
               "psnr_vs_ref": round(float(np.mean(ps)), 3), "ssim_vs_ref": round(float(np.mean(ss)), 5),
               "psnr_vs_ref_per_image": [round(float(x), 3) for x in ps],
               "ssim_vs_ref_per_image": [round(float(x), 5) for x in ss],
-              "psnr_gt": {k: round(v[0], 4) for k, v in mean_gt.items()},
-              "ssim_gt": {k: round(v[1], 5) for k, v in mean_gt.items()},
+              "psnr_gt": {k: round(v[0], 5) for k, v in mean_gt.items()},
+              "ssim_gt": {k: round(v[1], 6) for k, v in mean_gt.items()},
+              "per_image_vs_cpu_ref": per_img_d,
               "psnr_ssim_3sf": {k: [sf3(v[0]), sf3(v[1])] for k, v in mean_gt.items()},
               "psnr_ssim_3sf_match": match,
-              "note": "psnr/ssim_vs_ref: GPU bf16 output against the CPU fp32 reference output (metrics.py = "
-                      "skimage 0.18.3 restatement); psnr_gt / ssim_gt: each output against the clean image, mean over "
-                      "the images; psnr_ssim_3sf_match: an engine's mean PSNR and SSIM equal the CPU reference's at 3 "
-                      "significant figures (a miss is reported as false, not rounded away)"}
+              "note": "psnr/ssim_vs_ref: the bench engine's output (bf16 UNet + CLIP, fp16 VAE) against the CPU fp32 "
+                      "reference output (metrics.py = skimage 0.18.3 restatement); psnr_gt / ssim_gt: each output "
+                      "against the clean image, mean over the images; per_image_vs_cpu_ref: per image |PSNR - "
+                      "PSNR_ref| / |SSIM - SSIM_ref| (both against the clean image); psnr_ssim_3sf_match: an engine's "
+                      "mean PSNR and SSIM equal the CPU reference's at 3 significant figures (a miss is reported as "
+                      "false, not rounded away)"}
     return cpu, parity
 
 
@@ -285,6 +303,7 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's shard)")
     ap.add_argument("--sched-steps", type=int, default=50)
     ap.add_argument("--dtype", default=None, help="bf16 | fp16 | fp32 (default: the config's)")
+    ap.add_argument("--vae-dtype", default=None, help="VAE compute type (default: the task's, fp16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-images", type=int, default=4, help="configs[0] images for the CPU baseline (configs[0]: 4)")
     ap.add_argument("--no-roofline", action="store_true")
@@ -293,6 +312,7 @@ def main():
     spec = TASKS[args.task]
     batch = args.batch or spec["batch"]
     dtype = args.dtype or spec["dtype"]
+    vae_dtype = args.vae_dtype or (spec["vae"] if dtype != "fp32" else "fp32")
     res = spec["res"]
 
     rank, world, local = D.init()
@@ -308,13 +328,14 @@ def main():
     cfg = PipelineConfig.default(args.task)
     cfg.scheduler.kind = "ddim"          # BASELINE.json: "50 DDIM steps" (explicit override of the saved PNDM)
     t_init = time.perf_counter()
-    eng, sds, bcast = build_engine(cfg, dtype, device, rank)
+    eng, sds, bcast = build_engine(cfg, dtype, device, rank, vae_dtype)
     u8_h, mask_h = task_inputs(args.task, spec, batch, seed=rank)
     imgs = torch.from_numpy(u8_h).to(device).contiguous()
     mask = torch.from_numpy(mask_h).to(device).contiguous() if mask_h is not None else None
     noise = draw_noise(42, res // 8, res // 8, 2)
     prompt = PROMPTS[args.task]
-    log(f"[rank {rank}] engine ready in {time.perf_counter() - t_init:.1f}s ({args.task}, {dtype}, batch {batch})")
+    log(f"[rank {rank}] engine ready in {time.perf_counter() - t_init:.1f}s ({args.task}, {dtype}, VAE {vae_dtype}, "
+        f"batch {batch})")
 
     def step():
         eng._ctx_cache.clear()              # text encoding is part of every pass
@@ -378,7 +399,7 @@ def main():
         if args.task != "denoise":
             dn = PipelineConfig.default("denoise")
             sds = {k: W.random_state_dict(k, getattr(dn, k), 0) for k in ("unet", "vae", "clip")}
-            eng = SDEngine(dn, "bf16", device, state_dicts=sds)
+            eng = SDEngine(dn, "bf16", device, state_dicts=sds, vae_dtype="fp16")
         cpu, parity = cpu_baseline_and_parity(eng, sds, device, args.cpu_images, usable_cpus())
 
     if rank == 0:
@@ -394,6 +415,7 @@ def main():
                                                  if cfg_f == 2 else "no CFG")
                                    + (", 9-channel UNet, 2 VAE encodes" if args.task == "inpaint" else ""),
                        "task": args.task, "global_batch": batch * world, "resolution": res,
+                       "compute": f"UNet + CLIP {dtype}, VAE {vae_dtype} (fp32 accumulation)",
                        "parallelism": f"dp{world}", "weights_bcast": bcast,
                        "tflop_per_image": round(tflop_img, 2),
                        "achieved_tflops_end_to_end": round(value * tflop_img, 1), "outputs_finite": finite},

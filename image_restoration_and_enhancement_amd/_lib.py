@@ -124,6 +124,11 @@ _SIGS = {
     "irx_op_gn_conv3_ws_bytes": (sz, [i32, i32, i32, i32]),
     "irx_op_gn_conv3": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp, i64,
                               vp, vp, vp, vp]),
+    "irx_op_gn_conv_narrow": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp, i32, i32,
+                                    vp]),
+    "irx_op_gn_proj_ws_bytes": (sz, [i32, i32, i32, i32, i32]),
+    "irx_op_gn_proj": (i32, [vp, i32, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, i32, vp, vp, C.POINTER(i32),
+                             C.POINTER(i32)]),
     "irx_op_layer_norm": (i32, [vp, i32, vp, i32, i32, f32, vp, vp, vp]),
     "irx_op_attention": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp,
                                i64, i64, f32, i32]),

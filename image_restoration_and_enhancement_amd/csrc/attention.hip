@@ -280,233 +280,6 @@ __global__ __launch_bounds__(256, 1) void attn_kernel(AttnArgs a) {
   }
 }
 
-// max over lanes {i, i^16, i^32, i^48} with gfx950's v_permlane16/32_swap (VALU, no LDS round trip as
-// ds_bpermute would take): swapping a value with itself leaves each lane holding its partner's copy
-__device__ __forceinline__ float quad_max(float x) {
-  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
-}
-
-// ------------------------------------------------------------------------------------------------
-// bf16 throughput kernel: v_mfma_f32_16x16x32_bf16 for both products.
-//   S^T = K Q^T : K fragments by ds_read_b128 (d padded to DQ, a multiple of 32), Q^T in registers.
-//   O^T += V^T P^T over 32-key chunks: P^T is the exponentiated S^T accumulator of two 16-key tiles
-//   (lane group g holds keys 4g..4g+3 of each), V^T comes from two ds_read_b64_tr_b16 of the same
-//   key sets, so the permuted k order matches on both operands.
-// KT keys per LDS tile (128 at d <= 80, 64 at d = 160 to bound registers); 4 waves x 32 queries.
-// ONES: the head dim leaves a zero pad column in V (d < DV); it is set to 1 so the PV MFMAs also produce
-// the softmax row sums (O^T row d = sum_k P[q][k]) and the per-score VALU add disappears.
-template <int DQ, int DV, int KT, bool ONES, int OCC = 2>
-__global__ __launch_bounds__(256, OCC) void attn2_kernel(AttnArgs a) {
-  constexpr int SK = DQ + 8;                                     // 16 rows x b128 reads conflict-free
-  constexpr int SV = ((DV * 2 / 32) % 2 == 1) ? DV : DV + 16;    // 8 rows x 32 B tr reads conflict-free
-  // QK^T contracts over DQ = 32 * NDC (head dim zero-padded).  (A 16x16x16 MFMA for a d % 32 == 8..16 tail was
-  // tried: hipcc (ROCm 7.2) issues it right behind the 16x16x32 producing its accumulator with no wait states,
-  // and the result is wrong — mixed-shape MFMA accumulation chains are avoided here.)
-  // DQ % 32 == 16 (d = 40 -> 48): the last 16 dims go through one 16x16x16 MFMA into a SEPARATE
-  // accumulator that the VALU adds to S (no mixed-shape MFMA chain), instead of padding d to 64.
-  constexpr int NDC = DQ / 32, NDT = DV / 16, NKT = KT / 16, NKC = KT / 32;
-  constexpr bool TAIL = DQ % 32 == 16;
-  static_assert(DQ % 32 == 0 || TAIL, "head dim padding");
-  typedef __attribute__((ext_vector_type(8))) short s16x8;
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[KT * SK];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[KT * SV];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int li = lane & 15, g = lane >> 4;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int qb0 = blockIdx.x * kQB;
-  const int q0 = qb0 + wave * (kQT * 16);
-  const int d = a.d;
-  const bf16_t* __restrict__ Q = (const bf16_t*)a.q + (long)b * a.sq + (long)h * (a.hsq ? a.hsq : d);
-  const bf16_t* __restrict__ K = (const bf16_t*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : d);
-  const bf16_t* __restrict__ V = (const bf16_t*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : d);
-
-  for (int i = tid; i < KT * SK; i += 256) Ks[i] = 0;
-  for (int i = tid; i < KT * SV; i += 256) Vs[i] = (ONES && i % SV == a.d) ? (bf16_t)0x3F80 : (bf16_t)0;
-
-  s16x8 qf[kQT][NDC];
-  s16x4 qtl[kQT];
-#pragma unroll
-  for (int qt = 0; qt < kQT; ++qt) {
-    const int q = q0 + qt * 16 + li;
-#pragma unroll
-    for (int dc = 0; dc < NDC; ++dc) {
-      const int e = dc * 32 + 8 * g;
-      s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (q < a.Lq && e < d) v = *(const s16x8*)(Q + (long)q * a.ldq + e);
-      qf[qt][dc] = v;
-    }
-    qtl[qt] = s16x4{0, 0, 0, 0};
-    if constexpr (TAIL) {
-      const int e = NDC * 32 + 4 * g;
-      if (q < a.Lq && e < d) qtl[qt] = *(const s16x4*)(Q + (long)q * a.ldq + e);
-    }
-  }
-  f32x4 o[NDT][kQT];
-#pragma unroll
-  for (int i = 0; i < NDT; ++i)
-#pragma unroll
-    for (int j = 0; j < kQT; ++j) o[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float mrow[kQT], lrow[kQT];
-#pragma unroll
-  for (int j = 0; j < kQT; ++j) { mrow[j] = -INFINITY; lrow[j] = 0.f; }
-
-  const float sl2 = a.q_scaled ? 1.f : a.scale * 1.4426950408889634f;
-  int kend = a.Lk;
-  if (a.causal) kend = min(kend, qb0 + kQB);
-  const int cpr = d / 8;                                   // 16-byte chunks per K/V row
-  constexpr int NCH = (KT * (DV / 8) + 255) / 256;       // d <= DV
-  uint4 kreg[NCH], vreg[NCH];
-  auto load_regs = [&](int j0) {
-#pragma unroll
-    for (int u = 0; u < NCH; ++u) {
-      const int idx = tid + 256 * u;
-      kreg[u] = make_uint4(0, 0, 0, 0);
-      vreg[u] = make_uint4(0, 0, 0, 0);
-      if (idx < KT * cpr) {
-        const int r = idx / cpr, c = idx - r * cpr;
-        if (j0 + r < a.Lk) {
-          kreg[u] = *(const uint4*)(K + (long)(j0 + r) * a.ldk + c * 8);
-          vreg[u] = *(const uint4*)(V + (long)(j0 + r) * a.ldv + c * 8);
-        }
-      }
-    }
-  };
-  load_regs(0);
-
-  for (int j0 = 0; j0 < kend; j0 += KT) {
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < NCH; ++u) {
-      const int idx = tid + 256 * u;
-      if (idx < KT * cpr) {
-        const int r = idx / cpr, c = idx - r * cpr;
-        *(uint4*)(Ks + r * SK + c * 8) = kreg[u];
-        uint2* pv = (uint2*)(Vs + r * SV + c * 8);
-        pv[0] = make_uint2(vreg[u].x, vreg[u].y);
-        pv[1] = make_uint2(vreg[u].z, vreg[u].w);
-      }
-    }
-    __syncthreads();
-    if (j0 + KT < kend) load_regs(j0 + KT);
-
-    f32x4 s[NKT][kQT];
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-      for (int qt = 0; qt < kQT; ++qt) s[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int dc = 0; dc < NDC; ++dc) {
-        const s16x8 kf = *(const s16x8*)(Ks + (kt * 16 + li) * SK + dc * 32 + 8 * g);
-#pragma unroll
-        for (int qt = 0; qt < kQT; ++qt)
-          s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf),
-                                                              __builtin_bit_cast(bf16x8, qf[qt][dc]), s[kt][qt], 0, 0, 0);
-      }
-      if constexpr (TAIL) {
-        const s16x4 kt4 = *(const s16x4*)(Ks + (kt * 16 + li) * SK + NDC * 32 + 4 * g);
-#pragma unroll
-        for (int qt = 0; qt < kQT; ++qt) {
-          const f32x4 t = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kt4, qtl[qt], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          s[kt][qt] += t;
-        }
-      }
-    }
-
-    const bool need_mask = (j0 + KT > a.Lk) || (a.causal && j0 + KT - 1 > q0);
-    float nbq[kQT];
-#pragma unroll
-    for (int qt = 0; qt < kQT; ++qt) {
-      const int q = q0 + qt * 16 + li;
-      if (need_mask) {
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int key = j0 + kt * 16 + 4 * g + i;
-            if (key >= a.Lk || (a.causal && key > q)) s[kt][qt][i] = -INFINITY;
-          }
-      }
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < NKT; ++kt)
-        tmax = fmaxf(tmax, fmaxf(fmaxf(s[kt][qt][0], s[kt][qt][1]), fmaxf(s[kt][qt][2], s[kt][qt][3])));
-      tmax = quad_max(tmax);
-      const float mnew = fmaxf(mrow[qt], tmax);
-      const bool none = mnew == -INFINITY;
-      const float alpha = none ? 1.f : __builtin_amdgcn_exp2f((mrow[qt] - mnew) * sl2);
-      nbq[qt] = none ? 0.f : -mnew * sl2;
-      mrow[qt] = mnew;
-      if constexpr (!ONES) lrow[qt] *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) o[dt][qt] *= alpha;
-    }
-
-    // per 32-key chunk: exponentiate into the B operand, then its PV MFMAs (keeps 1 chunk of P live)
-#pragma unroll
-    for (int c = 0; c < NKC; ++c) {
-      s16x8 pf[kQT];
-#pragma unroll
-      for (int qt = 0; qt < kQT; ++qt) {
-        float lsum = 0.f;
-#pragma unroll
-        for (int half = 0; half < 2; ++half)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float p = __builtin_amdgcn_exp2f(fmaf(s[2 * c + half][qt][i], sl2, nbq[qt]));
-            if constexpr (!ONES) lsum += p;
-            pf[qt][half * 4 + i] = (short)f2bf(p);
-          }
-        if constexpr (!ONES) lrow[qt] += lsum;
-      }
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const bf16_t* v1 = Vs + (c * 32 + 4 * g + (li >> 2)) * SV + dt * 16 + 4 * (li & 3);
-        const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)v1);
-        const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v1 + 16 * SV));
-        const s16x8 vf = {t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
-#pragma unroll
-        for (int qt = 0; qt < kQT; ++qt)
-          o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vf),
-                                                              __builtin_bit_cast(bf16x8, pf[qt]), o[dt][qt], 0, 0, 0);
-      }
-    }
-  }
-
-  bf16_t* __restrict__ O = (bf16_t*)a.o + (long)b * a.so + (long)h * (a.hso ? a.hso : d);
-#pragma unroll
-  for (int qt = 0; qt < kQT; ++qt) {
-    float l;
-    if constexpr (ONES) {
-      // row d of O^T: tile dt1 = d/16, lane group (d%16)/4, element d%4 (d % 4 == 0: element 0)
-      float v = 0.f;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-        if (dt == d / 16) v = o[dt][qt][0];
-      l = __shfl(v, li + 16 * ((d % 16) / 4));
-    } else {
-      l = lrow[qt];
-      l += __shfl_xor(l, 16);
-      l += __shfl_xor(l, 32);
-    }
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    const int q = q0 + qt * 16 + li;
-    if (q >= a.Lq) continue;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-      const int e = dt * 16 + 4 * g;
-      if (e >= d) continue;
-      s16x4 v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (short)f2bf(o[dt][qt][i] * inv);
-      *(s16x4*)(O + (long)q * a.ldo + e) = v;
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // attn3: bf16 / fp16 flash attention on v_mfma_f32_32x32x16 (the shape that holds the SIMD's VALU issue
 // for 8 of its 32 cycles instead of 8 of 16 — this kernel is bounded by the softmax VALU work at d = 40).
@@ -1095,273 +868,6 @@ __global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// attn3p: attn3 (non-causal, K/V streamed) with the QK^T MFMAs of key tile j+1 issued ahead of tile j's softmax, so
-// inside one wave the matrix pipe computes S(j+1) while the vector unit runs tile j's row max / exp / convert, then
-// tile j's PV MFMAs follow (software pipelining across key tiles; attn3 runs MFMA -> VALU -> MFMA serially per wave
-// and relies on the other waves of the SIMD for overlap, measured MFMA busy 0.43 at d = 40).
-//   K is staged one tile ahead of V: the K stages hold tiles j+1 (read now) and j+2 (written at the end of the
-//   iteration), the V stages tiles j (read) and j+1 (written) — still two LDS stages per operand, one barrier per
-//   tile, K(j+2) / V(j+1) register-prefetched one iteration earlier.
-//   S(j+1) is formed with the running max of the time it is issued (-m in the Q pad column / accumulator
-//   initialisation); when tile j's deferred max moves m by delta, S(j+1) takes the same -delta as S(j).
-//   Two score accumulators alternate roles (the key loop is unrolled by two: no register copies).
-template <int D, int KT> constexpr int attn3p_occ() { return D <= 40 ? 2 : 1; }   // (3 at d = 40: 18 VGPRs spilled)
-
-template <typename T, int D, int KT>
-__global__ __launch_bounds__(256, (attn3p_occ<D, KT>())) void attn3p_kernel(AttnArgs a) {
-  constexpr int QB = 128;                                  // queries per block (4 waves x 32)
-  constexpr int DQ = (D + 15) / 16 * 16, NS = DQ / 16;     // QK^T contraction, 16-deep k-steps
-  constexpr int NDT = (D + 31) / 32;                       // 32-row tiles of O^T
-  constexpr bool ONES = D % 32 != 0;
-  constexpr int DVP = NDT * 32;
-  constexpr int SK = ((DQ / 8) % 2 == 0) ? DQ + 8 : DQ;
-  constexpr int SV = (DVP % 128 == 32 || DVP % 128 == 96) ? DVP : DVP + 32;
-  constexpr int NSUB = KT / 32;
-  constexpr int CPR = D / 8;
-  constexpr int NCH = (KT * CPR + 255) / 256;
-  constexpr float THR = 8.f;
-  static_assert(D % 8 == 0 && KT % 32 == 0, "attn3p shape");
-  __shared__ __attribute__((aligned(16))) uint16_t Ks2[2 * KT * SK];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs2[2 * KT * SV];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, hh = lane >> 5, g = lane >> 4;
-  const int nq = (a.Lq + QB - 1) / QB;
-  const int nblk = nq * a.H * a.B;
-  const int lid = a.xcd ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
-  const int qb = lid % nq, bh = lid / nq;
-  const int b = bh / a.H, h = bh - b * a.H;
-  const T* __restrict__ Q = (const T*)a.q + (long)b * a.sq + (long)h * (a.hsq ? a.hsq : D);
-  const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : D);
-  const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : D);
-
-  for (int i = tid; i < 2 * KT * SK; i += 256) Ks2[i] = (DQ > D && i % SK == D) ? one_bits<T>() : (uint16_t)0;
-  for (int i = tid; i < 2 * KT * SV; i += 256) Vs2[i] = (ONES && i % SV == D) ? one_bits<T>() : (uint16_t)0;
-
-  uint4 kreg[NCH], vreg[NCH];
-  const T* kp[NCH];
-  const T* vp[NCH];
-  int krow[NCH], ksoff[NCH], vsoff[NCH];
-#pragma unroll
-  for (int u = 0; u < NCH; ++u) {
-    const int idx = min(tid + 256 * u, KT * CPR - 1);
-    const int row = idx / CPR, c = idx - row * CPR;
-    krow[u] = row;
-    kp[u] = K + (long)row * a.ldk + c * 8;
-    vp[u] = V + (long)row * a.ldv + c * 8;
-    ksoff[u] = row * SK + c * 8;
-    vsoff[u] = row * SV + c * 8;
-  }
-  auto slot_ok = [&](int u) { return u < NCH - 1 || tid + 256 * u < KT * CPR; };
-  auto load1 = [&](int j0, const T* const* pp, long ld, uint4* reg) {
-    const long o = (long)j0 * ld;
-    if (j0 + KT <= a.Lk) {
-#pragma unroll
-      for (int u = 0; u < NCH; ++u)
-        if (slot_ok(u)) reg[u] = *(const uint4*)(pp[u] + o);
-    } else {
-#pragma unroll
-      for (int u = 0; u < NCH; ++u)
-        reg[u] = j0 + krow[u] < a.Lk ? *(const uint4*)(pp[u] + o) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto loadK = [&](int j0) { load1(j0, kp, a.ldk, kreg); };
-  auto loadV = [&](int j0) { load1(j0, vp, a.ldv, vreg); };
-  auto stageK = [&](int buf) {
-#pragma unroll
-    for (int u = 0; u < NCH; ++u)
-      if (slot_ok(u)) *(uint4*)(Ks2 + buf * KT * SK + ksoff[u]) = kreg[u];
-  };
-  auto stageV = [&](int buf) {
-#pragma unroll
-    for (int u = 0; u < NCH; ++u)
-      if (slot_ok(u)) *(uint4*)(Vs2 + buf * KT * SV + vsoff[u]) = vreg[u];
-  };
-
-  const int q0 = qb * QB + wave * 32;
-  const int qrow = q0 + r;
-  uint4 qf[NS];
-  const float sl2 = a.scale * 1.4426950408889634f;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int e = 16 * s + 8 * hh;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (qrow < a.Lq && e < D) v = *(const uint4*)(Q + (long)qrow * a.ldq + e);
-    if (!a.q_scaled) {
-      float f[8];
-      Vec16<T>::unpack(v, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] *= sl2;
-      v = Vec16<T>::pack(f);
-    }
-    qf[s] = v;
-  }
-  f32x16 oacc[NDT];
-#pragma unroll
-  for (int i = 0; i < NDT; ++i)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) oacc[i][k] = 0.f;
-  constexpr bool PADM = DQ > D;
-  constexpr int PADS = D / 16, PADE = (D % 16) - 8;
-  static_assert(!PADM || (D % 16 == 8 && PADE == 0), "pad column at element 0 of lane half 1");
-  float m = 0.f, lsum = 0.f;
-  bool first = true;
-  auto set_qpad = [&]() {
-    if constexpr (PADM) {
-      if (hh) qf[PADS].x = (qf[PADS].x & 0xFFFF0000u) | (Mfma<T>::pack2(-m, 0.f) & 0xFFFFu);
-    }
-  };
-  // S'^T = K Q^T - m (m as of now) for the K tile in stage `ks`
-  auto qk = [&](int ks, f32x16* sacc) {
-    const uint16_t* Ks = Ks2 + ks * KT * SK;
-    const float init = (PADM || first) ? 0.f : -m;
-#pragma unroll
-    for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-      for (int k = 0; k < 16; ++k) sacc[c][k] = init;
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-#pragma unroll
-      for (int c = 0; c < NSUB; ++c) {
-        const uint4 kf = *(const uint4*)(Ks + (c * 32 + r) * SK + 16 * s + 8 * hh);
-        sacc[c] = Mfma<T>::m32x32x16(kf, qf[s], sacc[c]);
-      }
-  };
-  const int ntile = (a.Lk + KT - 1) / KT;
-  // one key tile: S(it + 1) issued first (into sn), then tile it's softmax on sc and its PV, then the staging
-  auto body = [&](int it, f32x16* sc, f32x16* sn) {
-    const int j0 = it * KT;
-    const bool nxt = it + 1 < ntile;
-    if (nxt) qk((it + 1) & 1, sn);
-    if (j0 + KT > a.Lk) {
-#pragma unroll
-      for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const int key = j0 + 32 * c + (k & 3) + 8 * (k >> 2) + 4 * hh;
-          if (key >= a.Lk) sc[c][k] = -INFINITY;
-        }
-    }
-    float mx[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) mx[t] = fmaxf(sc[0][4 * t], sc[0][4 * t + 1]);
-#pragma unroll
-    for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int k = (c == 0 ? 2 : 0); k < 4; k += 2)
-          mx[t] = fmaxf(fmaxf(mx[t], sc[c][4 * t + k]), sc[c][4 * t + k + 1]);
-    float tmax = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
-    tmax = fmaxf(tmax, xlane32(tmax));
-    if (first || __any(tmax > THR)) {
-      const float tgt = first ? (tmax == -INFINITY ? 0.f : m + tmax) : m + fmaxf(tmax, 0.f);
-      const float mn = Mfma<T>::round(tgt);
-      const float delta = mn - m;
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-#pragma unroll
-      for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-        for (int k = 0; k < 16; ++k) sc[c][k] -= delta;
-      if (nxt) {   // S(it + 1) was formed with the old m
-#pragma unroll
-        for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-          for (int k = 0; k < 16; ++k) sn[c][k] -= delta;
-      }
-      if (!first) {
-#pragma unroll
-        for (int i = 0; i < NDT; ++i)
-#pragma unroll
-          for (int k = 0; k < 16; ++k) oacc[i][k] *= alpha;
-        if constexpr (!ONES) lsum *= alpha;
-      }
-      m = mn;
-      first = false;
-      set_qpad();
-    }
-    const uint16_t* Vs = Vs2 + (it & 1) * KT * SV;
-#pragma unroll
-    for (int c = 0; c < NSUB; ++c) {
-      uint4 pb[2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        float p[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          p[j] = __builtin_amdgcn_exp2f(sc[c][8 * s2 + j]);
-          if constexpr (!ONES) lsum += p[j];
-        }
-        pb[s2] = make_uint4(Mfma<T>::pack2(p[0], p[1]), Mfma<T>::pack2(p[2], p[3]), Mfma<T>::pack2(p[4], p[5]),
-                            Mfma<T>::pack2(p[6], p[7]));
-      }
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int krow2 = 32 * c + 16 * s2 + 4 * (g >> 1) + ((lane & 15) >> 2);
-          const int col = 32 * dt + 16 * (g & 1) + 4 * (lane & 3);
-          const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + krow2 * SV + col));
-          const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + (krow2 + 8) * SV + col));
-          const uint4 vf = make_uint4(__builtin_bit_cast(uint2, t1).x, __builtin_bit_cast(uint2, t1).y,
-                                      __builtin_bit_cast(uint2, t2).x, __builtin_bit_cast(uint2, t2).y);
-          oacc[dt] = Mfma<T>::m32x32x16(vf, pb[s2], oacc[dt]);
-        }
-    }
-    // K(it + 2) into the stage S(it) was read from (iteration it - 1), V(it + 1) into the stage PV(it - 1) read
-    if (it + 2 < ntile) stageK(it & 1);
-    if (nxt) stageV((it + 1) & 1);
-    __syncthreads();
-    if (it + 3 < ntile) loadK((it + 3) * KT);
-    if (it + 2 < ntile) loadV((it + 2) * KT);
-  };
-
-  // prologue: K0 / V0 staged, S(0) formed, K1 staged; kreg = K2, vreg = V1
-  loadK(0);
-  loadV(0);
-  __syncthreads();              // pad-column initialisation complete
-  stageK(0);
-  stageV(0);
-  if (ntile > 1) {
-    loadK(KT);
-    loadV(KT);
-  }
-  __syncthreads();
-  f32x16 sa[NSUB], sb[NSUB];
-  qk(0, sa);
-  if (ntile > 1) stageK(1);
-  if (ntile > 2) loadK(2 * KT);
-  __syncthreads();
-  for (int it = 0; it < ntile; it += 2) {
-    body(it, sa, sb);
-    if (it + 1 < ntile) body(it + 1, sb, sa);
-  }
-
-  float l;
-  if constexpr (ONES) {
-    constexpr int dts = D / 32, rho = D % 32, hs = (rho >> 2) & 1, reg = (rho & 3) + 4 * (rho >> 3);
-    const float v = oacc[dts][reg];
-    const float o = xlane32(v);
-    l = hh == hs ? v : o;
-  } else {
-    l = lsum + xlane32(lsum);
-  }
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  if (qrow < a.Lq) {
-    T* __restrict__ O = (T*)a.o + (long)b * a.so + (long)h * (a.hso ? a.hso : D) + (long)qrow * a.ldo;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = 32 * dt + 8 * k + 4 * hh;
-        if (e >= D) continue;
-        *(uint2*)(O + e) = make_uint2(Mfma<T>::pack2(oacc[dt][4 * k] * inv, oacc[dt][4 * k + 1] * inv),
-                                      Mfma<T>::pack2(oacc[dt][4 * k + 2] * inv, oacc[dt][4 * k + 3] * inv));
-      }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // attnw: flash attention for wide heads (the VAE mid-block's single d = 512 head), bf16 / fp16, non-causal.
 // Block = 4 waves x the same 32 queries; wave w owns d-quarter w.  Per 32-key tile:
 //   partial S^T_w = K[:, d_w] Q[:, d_w]^T (D/64 k-steps of v_mfma_f32_32x32x16, K fragments straight from
@@ -1528,42 +1034,46 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
     while (qrep < 8 && ((a.Lq + 128 * 2 * qrep - 1) / (128 * 2 * qrep)) * a.H * a.B >= 1024) qrep *= 2;
   const int nq = (a.Lq + 128 * qrep - 1) / (128 * qrep);
   dim3 grid(nq * a.H * a.B), block(256);
-  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn3_kernel<") +
-                               (std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short") + ", " +
-                               std::to_string(D) + ", " + std::to_string(KT) + ", " + (CAUSAL ? "true" : "false") + (res ? ", true" : ", false") + ">" +
-                               (g_prof_shapes ? " [B " + std::to_string(a.B) + " Lq " + std::to_string(a.Lq) + " Lk " +
-                                                    std::to_string(a.Lk) + "]"
-                                              : std::string())
-                         : std::string(),
-               4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
+  // which kernel runs: resident K/V (cross-attention), two query groups per wave (d = 40 self), the prefetching
+  // attn3 (PF 3), or plain attn3; the profiler names the launch as rocprofv3 demangles it
+  enum { kRes, kQ2, kPf, kPlain };
+  int kind = kPlain;
+  if (!CAUSAL && res) kind = kRes;
+  else if (!CAUSAL && D == 40 && g_attn_q2) kind = kQ2;
+  else if (!CAUSAL && D == 40 && g_attn_pf) kind = kPf;
+  std::string nm;
+  if (prof_on()) {
+    const std::string tn = std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short";
+    nm = kind == kQ2 ? "irx::(anonymous namespace)::attn3q_kernel<" + tn + ", " + std::to_string(D) + ", " +
+                           std::to_string(KT) + ">"
+                     : "irx::(anonymous namespace)::attn3_kernel<" + tn + ", " + std::to_string(D) + ", " +
+                           std::to_string(KT) + ", " + (CAUSAL ? "true" : "false") + ", " +
+                           (kind == kRes ? "true" : "false") + ", " + (kind == kPf ? "3" : "0") + ">";
+    if (g_prof_shapes)
+      nm += " [B " + std::to_string(a.B) + " Lq " + std::to_string(a.Lq) + " Lk " + std::to_string(a.Lk) + "]";
+  }
+  ProfScope ps(nm, 4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
   AttnArgs b = a;
   b.xcd = g_attn_xcd;
   b.prio = g_attn_prio;
   b.qrep = qrep;
   if constexpr (!CAUSAL) {
-    if (res) {
+    if (kind == kRes) {
       attn3_kernel<T, D, KT, false, true><<<grid, block, 0, s>>>(b);
       IRX_LAUNCH_CHECK();
       return;
     }
     if constexpr (D == 40) {
-      if (g_attn_pipe) {   // (ProfScope above names attn3: the A/B is read from the timing, not the name)
-        attn3p_kernel<T, D, KT><<<grid, block, 0, s>>>(b);
+      if (kind == kQ2) {
+        attn3q_kernel<T, D, KT><<<dim3(((a.Lq + 255) / 256) * a.H * a.B), block, 0, s>>>(b);
         IRX_LAUNCH_CHECK();
         return;
       }
-    }
-  }
-  if constexpr (!CAUSAL && D == 40) {
-    if (g_attn_q2) {   // two 32-query groups per wave (ProfScope above names attn3: the A/B is read from the timing)
-      attn3q_kernel<T, D, KT><<<dim3(((a.Lq + 255) / 256) * a.H * a.B), block, 0, s>>>(b);
-      IRX_LAUNCH_CHECK();
-      return;
-    }
-    if (g_attn_pf) {   // (ProfScope above names attn3: the A/B is read from the timing, not the name)
-      attn3_kernel<T, D, KT, false, false, 3><<<grid, block, 0, s>>>(b);
-      IRX_LAUNCH_CHECK();
-      return;
+      if (kind == kPf) {
+        attn3_kernel<T, D, KT, false, false, 3><<<grid, block, 0, s>>>(b);
+        IRX_LAUNCH_CHECK();
+        return;
+      }
     }
   }
   attn3_kernel<T, D, KT, CAUSAL, false><<<grid, block, 0, s>>>(b);
@@ -1586,33 +1096,6 @@ bool launch3(const AttnArgs& a, hipStream_t s) {
     case 160: launch3_d<T, 160>(a, s); return true;
     default: return false;
   }
-}
-
-void launch_bf16(const AttnArgs& a, hipStream_t s) {
-  dim3 grid((a.Lq + kQB - 1) / kQB, a.H, a.B), block(256);
-  const char* inst = a.d == 40 ? (g_attn_d40 == 1   ? "64, 48, 128, false"
-                                  : g_attn_d40 == 2 ? "64, 48, 64, true, 3"
-                                  : g_attn_d40 == 3 ? "64, 48, 64, true, 4"
-                                  : g_attn_d40 == 4 ? "48, 48, 64, true, 3"
-                                                    : "64, 48, 128, true, 2")
-                     : a.d == 64 ? "64, 64, 128, false"
-                     : a.d == 80 ? "96, 80, 64, false" : "160, 160, 32, false";
-  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::attn2_kernel<") + inst + ">" : std::string(),
-               4.0 * a.B * a.H * (double)a.Lq * a.Lk * a.d, s);
-  switch (a.d) {
-    case 40:
-      if (g_attn_d40 == 1) attn2_kernel<64, 48, 128, false><<<grid, block, 0, s>>>(a);
-      else if (g_attn_d40 == 2) attn2_kernel<64, 48, 64, true, 3><<<grid, block, 0, s>>>(a);
-      else if (g_attn_d40 == 3) attn2_kernel<64, 48, 64, true, 4><<<grid, block, 0, s>>>(a);
-      else if (g_attn_d40 == 4) attn2_kernel<48, 48, 64, true, 3><<<grid, block, 0, s>>>(a);
-      else attn2_kernel<64, 48, 128, true><<<grid, block, 0, s>>>(a);
-      break;
-    case 64: attn2_kernel<64, 64, 128, false><<<grid, block, 0, s>>>(a); break;
-    case 80: attn2_kernel<96, 80, 64, false><<<grid, block, 0, s>>>(a); break;
-    case 160: attn2_kernel<160, 160, 32, false><<<grid, block, 0, s>>>(a); break;
-    default: throw Error("attention: unsupported head dim " + std::to_string(a.d));
-  }
-  IRX_LAUNCH_CHECK();
 }
 
 template <typename T>
@@ -1653,21 +1136,15 @@ void attention(const AttnArgs& a, hipStream_t s) {
   if (a.dtype == F32) launch_t<float>(a, s);
   else if (a.dtype == F16) {
     IRX_CHECK(v16 && launch3<f16_t>(a, s), "fp16 attention: head dim must be 40 / 64 / 80 / 160 with 16-byte rows");
-  } else if (g_attn_v3 && v16 && launch3<bf16_t>(a, s)) {
-  } else if (g_attn_v2 && v16) launch_bf16(a, s);
-  else launch_t<bf16_t>(a, s);
+  } else if (!(v16 && launch3<bf16_t>(a, s))) {
+    launch_t<bf16_t>(a, s);
+  }
 }
-int g_attn_v3 = 1;
 int g_attn_q2 = 1;     // irx_set_option("attn_q2", 0): d = 40 self-attention with one query group per wave (attn3, A/B)
 int g_attn_pf = 1;     // irx_set_option("attn_pf", 0): d = 40 self-attention without the whole-tile fragment prefetch (A/B)
-int g_attn_pipe = 0;   // irx_set_option("attn_pipe", 1): d = 40 self-attention on attn3p (QK^T one key tile ahead; A/B)
 int g_attn_xcd = 1;
 int g_attn_prio = 0;
 int g_attn_qrep = 1;   // irx_set_option("attn_qrep", 0): one query group per block in cross-attention (A/B)   // irx_set_option("attn_prio", 1): MFMA chains of attn3 at raised wave priority (A/B)
 int g_attn_hm = 1;
-
-bool g_attn_v2 = true;
-int g_attn_d40 = 2;   // d = 40 variant (A/B): 0 128-key tiles (ones-column row sums), 1 VALU row sums,
-                      // 2/3 64-key tiles at 3/4 blocks per CU (2, default: +8% self, +40% cross-attention; 3 spills)
 
 }  // namespace irx

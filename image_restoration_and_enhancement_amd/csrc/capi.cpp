@@ -66,7 +66,6 @@ struct OptRef {
 };
 static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"large_tiles", nullptr, &g_large_tiles},
-    {"attn_v2", nullptr, &g_attn_v2},
     {"gemm_deep", &g_gemm_deep, nullptr},
     {"gemm_dbg", &g_gemm_dbg, nullptr},
     {"gn_v2", nullptr, &g_gn_v2},
@@ -74,7 +73,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gn_parts", &g_gn_parts, nullptr},
     {"ln_parts", &g_ln_parts, nullptr},
     {"gn_fold", &g_gn_fold, nullptr},
-    {"attn_pipe", &g_attn_pipe, nullptr},
+    {"gn_narrow", &g_gn_narrow, nullptr},
     {"attn_pf", &g_attn_pf, nullptr},
     {"attn_q2", &g_attn_q2, nullptr},
     {"halo_split", &g_halo_split, nullptr},
@@ -98,8 +97,6 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gemm_force", &g_gemm_force, nullptr},
     {"conv_halo", &g_conv_halo, nullptr},
     {"gemm_small", nullptr, &g_gemm_small},
-    {"attn_d40", &g_attn_d40, nullptr},
-    {"attn_v3", &g_attn_v3, nullptr},
     {"attn_xcd", &g_attn_xcd, nullptr},
     {"attn_hm", &g_attn_hm, nullptr},
     {"gemm_small_kmax", &g_gemm_small_kmax, nullptr},
@@ -617,6 +614,67 @@ int irx_op_gn_conv3(void* s, int dtype, const void* x0, const void* x1, int c0, 
   a.gn_ab = ab;
   a.gn_silu = silu;
   gemm(a, S(s));
+  IRX_API_END
+}
+
+// workspace of irx_op_gn_proj: statistics + (ab) + the normalised copy or the per-image folded weights / biases
+static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
+size_t irx_op_gn_proj_ws_bytes(int n, int hw, int groups, int k, int nout) {
+  const size_t big = std::max((size_t)n * hw * k, (size_t)n * nout * k) * 2;
+  return al256(gn_ws_bytes(n, hw, groups)) + al256((size_t)n * k * sizeof(float2)) + al256(big) +
+         al256((size_t)n * nout * sizeof(float));
+}
+
+int irx_op_gn_proj(void* s, int dtype, const void* x, int n, int hw, int k, int groups, float eps, const float* gamma,
+                   const float* beta, const void* w, const float* bias, int nout, void* out, void* ws, int* folded,
+                   int* splits) {
+  IRX_API_BEGIN
+  IRX_CHECK(folded && splits, "null argument");
+  IRX_CHECK(dtype != F32, "irx_op_gn_proj: 16-bit engines only");
+  GemmArgs a;
+  a.dtype = dtype; a.M = n * hw; a.N = nout; a.K = k;
+  a.A = x; a.lda = k;
+  a.B = w; a.ldb = k;
+  a.C = out ? out : (void*)(uintptr_t)4096; a.ldc = nout;   // (query: an aligned stand-in, never written)
+  a.imgs = n;
+  a.b_rows = hw; a.b_img_stride = (long)nout * k; a.bias_img_stride = nout;
+  *folded = (g_gn_fold && gemm_bimg_ok(a)) ? 1 : 0;
+  if (!*folded) { a.b_rows = 0; a.b_img_stride = 0; a.bias_img_stride = 0; }
+  *splits = gemm_large_splits(a);
+  if (!out) return 0;
+  IRX_CHECK(x && gamma && beta && w && ws, "null buffer");
+  char* p = (char*)ws;
+  void* gws = p;
+  p += al256(gn_ws_bytes(n, hw, groups));
+  float2* ab = (float2*)p;
+  p += al256((size_t)n * k * sizeof(float2));
+  void* big = p;
+  p += al256(std::max((size_t)n * hw * k, (size_t)n * nout * k) * 2);
+  float* bo = (float*)p;
+  if (*folded) {   // the engine's form (models.cpp Unet::transformer), statistics from a pass instead of producer partials
+    group_norm_stats(dtype, x, nullptr, k, 0, n, hw, groups, eps, gamma, beta, ab, gws, S(s));
+    gn_fold_weights(dtype, w, bias, ab, beta, gn_mr_ws(gws, n, groups), groups, nout, k, n, big, bo, S(s));
+    a.B = big;
+    a.bias = bo;
+  } else {
+    group_norm(dtype, x, nullptr, k, 0, n, hw, groups, eps, gamma, beta, 0, big, gws, S(s));
+    a.A = big;
+    a.bias = bias;
+  }
+  gemm(a, S(s));
+  IRX_API_END
+}
+
+int irx_op_gn_conv_narrow(void* s, int dtype, const void* x, int n, int h, int w, int c, int groups, float eps,
+                          const float* gamma, const float* beta, int silu, const void* weight, const float* bias,
+                          int cout, void* out, int ldo, int out_f32, void* ws) {
+  IRX_API_BEGIN
+  IRX_CHECK(x && gamma && beta && weight && out && ws, "null buffer");
+  IRX_CHECK(gn_conv_narrow_ok(dtype, c, cout), "shape/dtype does not take the fused narrow conv (16-bit, C % 64 == 0)");
+  float2* ab = (float2*)ws;
+  void* gws = (char*)ws + gn_conv3_ab_bytes(n, c);
+  group_norm_stats(dtype, x, nullptr, c, 0, n, h * w, groups, eps, gamma, beta, ab, gws, S(s));
+  gn_conv_narrow(dtype, x, n, h, w, c, ab, silu, weight, bias, cout, out, ldo, out_f32, S(s));
   IRX_API_END
 }
 

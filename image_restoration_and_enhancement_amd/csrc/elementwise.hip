@@ -166,14 +166,32 @@ __global__ void latent_kernel(const T* __restrict__ mom, int mcs, long npix, lon
 template <typename T>
 __device__ __forceinline__ void pack_pixel(T* __restrict__ dst, const float* lat4, int cin_pad, int inpaint,
                                            const float* mask, const float* masked, long pix) {
-  int c = 0;
-  for (; c < 4; ++c) dst[c] = from_f<T>(lat4[c]);
-  if (inpaint) {
-    dst[4] = from_f<T>(mask[pix]);
-    for (int e = 0; e < 4; ++e) dst[5 + e] = from_f<T>(masked[pix * 4 + e]);
-    c = 9;
+  if constexpr (sizeof(T) == 2) {
+    // 16-bit engines: whole 16-byte chunks (cin_pad is 64 there: conv_in runs on the 64-channel-slab conv tiles)
+    alignas(16) T v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = T(0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = from_f<T>(lat4[e]);
+    if (inpaint) {
+      v[4] = from_f<T>(mask[pix]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[5 + e] = from_f<T>(masked[pix * 4 + e]);
+    }
+    uint4* d = (uint4*)dst;
+    d[0] = *(const uint4*)&v[0];
+    if (cin_pad >= 16) d[1] = *(const uint4*)&v[8];
+    for (int k = 2; k < cin_pad / 8; ++k) d[k] = uint4{0u, 0u, 0u, 0u};
+  } else {
+    int c = 0;
+    for (; c < 4; ++c) dst[c] = from_f<T>(lat4[c]);
+    if (inpaint) {
+      dst[4] = from_f<T>(mask[pix]);
+      for (int e = 0; e < 4; ++e) dst[5 + e] = from_f<T>(masked[pix * 4 + e]);
+      c = 9;
+    }
+    for (; c < cin_pad; ++c) dst[c] = T(0);
   }
-  for (; c < cin_pad; ++c) dst[c] = T(0);
 }
 
 template <typename T>

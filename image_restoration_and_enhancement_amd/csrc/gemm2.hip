@@ -28,6 +28,14 @@
 namespace irx {
 
 __device__ uint4 g_zero_page[4];   // 64 zero bytes: the source of every padded / out-of-range lane
+// Timing-diagnostic knock-outs (option gemm_dbg) exist only in the diagnostic build (scripts/build_stamps.sh:
+// -DIRX_DIAG / -DIRX_HALO_STAMPS, scripts/_skdbg/libirx_stamps.so); the product library compiles them out.
+#if defined(IRX_DIAG) || defined(IRX_HALO_STAMPS)
+constexpr int kDbgMask = ~0;
+#define IRX_HALO_DIAG 1
+#else
+constexpr int kDbgMask = 0;
+#endif
 #ifdef IRX_HALO_STAMPS
 constexpr int kHaloStampBlocks = 2048;
 __device__ unsigned long long g_halo_stamps[kHaloStampBlocks * 8 * 8];
@@ -620,7 +628,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       asm volatile("s_barrier" ::: "memory");   // everyone's pieces landed; everyone finished reading kt-1
       if (kt + S - 1 < nk) issueB(kt + S - 1, st == 0 ? S - 1 : st - 1);
       if (t == 0 && 9 * (c + 1) < nk) issueH(c + 1);
-      if (!(a.dbg & 2)) {
+      if (!(a.dbg & kDbgMask & 2)) {
         const int ky = t / 3, kx = t - 3 * ky;
         const int shift = ky * W + kx - 1;
         const uint4* Hs = Hb + (c & 1) * HB_U4;
@@ -789,7 +797,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       }
     };
     auto mma = [&]() {
-      if (a.dbg & 2) return;
+      if (a.dbg & kDbgMask & 2) return;
 #pragma unroll
       for (int s = 0; s < KSUB; ++s)
 #pragma unroll
@@ -833,7 +841,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     for (int kt = kt0; kt < kt1; ++kt) {
       const int st = (kt - kt0) & 1;
       if (kt + 1 < kt1) issue(kt + 1, st ^ 1);
-      if (!(a.dbg & 2)) compute(st);
+      if (!(a.dbg & kDbgMask & 2)) compute(st);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -848,14 +856,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       wait_vm(IPW * min(S - 2, kt1 - 1 - kt));
       asm volatile("s_barrier" ::: "memory");   // everyone's pieces landed; everyone finished reading kt-1
       if (kt + S - 1 < kt1) issue(kt + S - 1, st == 0 ? S - 1 : st - 1);
-      if (!(a.dbg & 2)) compute(st);
+      if (!(a.dbg & kDbgMask & 2)) compute(st);
       st = st + 1 == S ? 0 : st + 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  if (a.dbg & 1) {   // diagnostics: keep the accumulators live, skip the output
+  if (a.dbg & kDbgMask & 1) {   // diagnostics: keep the accumulators live, skip the output
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -1359,7 +1367,7 @@ void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
 
 template <int BM, int BN, int WM, int WN, int BK, int S, int HALO = 0, bool PP = false>
 void launch2(const GemmArgs& a, const Split& sp, hipStream_t s) {
-  if constexpr (HALO == 4) launch2_t<bf16_t, BM, BN, WM, WN, BK, S, HALO, PP>(a, sp, s);   // (bf16 diagnostics only)
+  if constexpr (HALO == 4) launch2_t<bf16_t, BM, BN, WM, WN, BK, S, HALO, PP>(a, sp, s);   // (bf16 diagnostic build)
   else if (a.dtype == F16) launch2_t<f16_t, BM, BN, WM, WN, BK, S, HALO, PP>(a, sp, s);
   else launch2_t<bf16_t, BM, BN, WM, WN, BK, S, HALO, PP>(a, sp, s);
 }
@@ -1578,6 +1586,16 @@ bool gemm_bimg_ok(const GemmArgs& a) {
   return g_gemm_pp != 1 && g_gemm_deep == 0;
 }
 
+int halo_splits(const GemmArgs& a, long tiles);
+
+// K splits the large-tile path would run `a` with (1: none; 0: not a large-tile shape) — for tests / diagnostics
+int gemm_large_splits(const GemmArgs& a) {
+  if (!g_large_tiles || !eligible(a) || gemm_sk_eligible(a)) return 0;
+  if (const int hbn = halo_bn(a)) return halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));
+  const Choice c = choose(a);
+  return c.BM ? c.splits : 0;
+}
+
 bool gemm_geglu_fusable(const GemmArgs& a) {
   if (!g_large_tiles || !a.geglu || !eligible(a) || !vec_ok(a)) return false;
   if (gemm_sk_eligible(a)) return true;
@@ -1667,8 +1685,11 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
       sp.inkernel = true;
       sp.cnt = stream_counters(s);
     }
+#ifdef IRX_HALO_DIAG
     if (g_halo_pipe && !a.gn_ab && b.dbg && a.dtype == BF16) launch2<256, 160, 4, 2, 64, 3, 4>(b, sp, s);   // (diagnostics)
-    else if (g_halo_pipe && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 2>(b, sp, s);   // ping-pong main loop
+    else
+#endif
+    if (g_halo_pipe && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 2>(b, sp, s);   // ping-pong main loop
     else launch2<256, 160, 4, 2, 64, 3, 1>(b, sp, s);
     return true;
   }

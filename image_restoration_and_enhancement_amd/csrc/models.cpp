@@ -217,6 +217,26 @@ void Model::gnorm(Ctx& c, const Act& x0, const Act* x1, P g, P b, float eps, int
   c.ws->free(ws);
 }
 
+bool Model::gn_conv_out(Ctx& c, const Act& x, P g, P gb, float eps, P w, P b, int cout, void* out, int ldo,
+                        int out_f32) {
+  if (!g_gn_narrow || !gn_conv_narrow_ok(dt_, x.c, cout)) return false;
+  const int HW = x.h * x.w;
+  float2* ab = (float2*)c.ws->alloc((size_t)x.n * x.c * sizeof(float2));
+  const bool parts = x.gnp && HW % x.gnr == 0;
+  void* ws = parts ? nullptr : c.ws->alloc(gn_ws_bytes(x.n, HW, cfg_.norm_groups));
+  if (!c.ws->dry()) {
+    if (parts)
+      group_norm_parts_ab(x.c, x.n, HW, cfg_.norm_groups, eps, fptr(g), fptr(gb), x.gnp, x.gnr, ab, nullptr, c.s);
+    else
+      group_norm_stats(dt_, x.p, nullptr, x.c, 0, x.n, HW, cfg_.norm_groups, eps, fptr(g), fptr(gb), ab, ws, c.s);
+    gn_conv_narrow(dt_, x.p, x.n, x.h, x.w, x.c, ab, 1, ptr(w), b.set ? fptr(b) : nullptr, cout, out, ldo, out_f32,
+                   c.s);
+  }
+  if (ws) c.ws->free(ws);
+  c.ws->free(ab);
+  return true;
+}
+
 void Model::lnorm(Ctx& c, const void* x, int rows, int C, P g, P b, float eps, void* out) {
   if (c.ws->dry()) return;
   layer_norm(dt_, x, C, rows, C, eps, fptr(g), fptr(b), out, C, c.s);
@@ -296,7 +316,9 @@ Unet::Unet(const irx_model_config& cfg, int dtype) : Model(IRX_MODEL_UNET, cfg, 
   IRX_CHECK(cfg.heads > 0 && cfg.norm_groups > 0, "bad UNet config");
   const int* bo = cfg.block_out_channels;
   const int nb = cfg.n_blocks;
-  cin_pad_ = (cfg.in_channels + 7) / 8 * 8;
+  // 16-bit engines: the input is padded to one 64-channel slab, so conv_in runs on the large-tile conv paths (the halo
+  // tiles at 64x64 latents) instead of the 4-wave kernel (zero channels cost MFMAs, not bandwidth: 75 -> ~20 us)
+  cin_pad_ = dtype != F32 ? (cfg.in_channels + 63) / 64 * 64 : (cfg.in_channels + 7) / 8 * 8;
   ln_fold_ = dtype != F32 && g_ln_fold;
   temb_dim_ = bo[0] * 4;
   conv_in_w = conv("conv_in.weight", bo[0], 3, 3, cin_pad_);
@@ -450,9 +472,10 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
     float2* ab = (float2*)c.ws->alloc((size_t)B * C * sizeof(float2));
     void* wf = c.ws->alloc((size_t)B * C * C * es);
     float* bf = (float*)c.ws->alloc((size_t)B * C * sizeof(float));
+    float2* mr = (float2*)c.ws->alloc((size_t)B * cfg_.norm_groups * sizeof(float2));
     if (!c.ws->dry()) {
-      group_norm_parts_ab(C, B, HW, cfg_.norm_groups, 1e-6f, fptr(a.nw), fptr(a.nb), x.gnp, x.gnr, ab, c.s);
-      gn_fold_weights(dt_, ptr(a.piw), fptr(a.pib), ab, C, C, B, wf, bf, c.s);
+      group_norm_parts_ab(C, B, HW, cfg_.norm_groups, 1e-6f, fptr(a.nw), fptr(a.nb), x.gnp, x.gnr, ab, mr, c.s);
+      gn_fold_weights(dt_, ptr(a.piw), fptr(a.pib), ab, fptr(a.nb), mr, cfg_.norm_groups, C, C, B, wf, bf, c.s);
     }
     pg.B = wf;
     pg.bias = bf;
@@ -463,6 +486,7 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
       parts = lnp;
     }
     run_gemm(c, pg);
+    c.ws->free(mr);
     c.ws->free(bf);
     c.ws->free(wf);
     c.ws->free(ab);
@@ -634,13 +658,18 @@ void Unet::run(Ctx& c, const void* x, int B, int h, int w, const float* t, const
       cur = u;
     }
   }
-  Act gn = new_act(c, B, h, w, bo[0]);
-  gnorm(c, cur, nullptr, nout_w, nout_b, eps, 1, gn);
-  drop(c, cur);
-  Act o;
-  o.p = eps_out; o.n = B; o.h = h; o.w = w; o.c = cfg_.out_channels;
-  conv2d(c, gn, nullptr, conv_out_w, conv_out_b, cfg_.out_channels, 3, 1, 1, 1, h, w, o, nullptr, 0, nullptr, 1);
-  drop(c, gn);
+  if (gn_conv_out(c, cur, nout_w, nout_b, eps, conv_out_w, conv_out_b, cfg_.out_channels, eps_out, cfg_.out_channels,
+                  1)) {
+    drop(c, cur);
+  } else {
+    Act gn = new_act(c, B, h, w, bo[0]);
+    gnorm(c, cur, nullptr, nout_w, nout_b, eps, 1, gn);
+    drop(c, cur);
+    Act o;
+    o.p = eps_out; o.n = B; o.h = h; o.w = w; o.c = cfg_.out_channels;
+    conv2d(c, gn, nullptr, conv_out_w, conv_out_b, cfg_.out_channels, 3, 1, 1, 1, h, w, o, nullptr, 0, nullptr, 1);
+    drop(c, gn);
+  }
   c.ws->free(tproj);
 }
 
@@ -877,12 +906,16 @@ void Vae::run_encode(Ctx& c, const void* img, int B, int H, int W, void* moments
   drop(c, r);
   cur = resnet(c, e_mid1_, a);
   drop(c, a);
-  Act gn = new_act(c, B, cur.h, cur.w, cur.c);
-  gnorm(c, cur, nullptr, e_nout_w, e_nout_b, cfg_.norm_eps, 1, gn);
-  drop(c, cur);
-  Act co = new_act(c, B, gn.h, gn.w, 8);
-  conv2d(c, gn, nullptr, e_cout_w, e_cout_b, 8, 3, 1, 1, 1, gn.h, gn.w, co);
-  drop(c, gn);
+  Act co = new_act(c, B, cur.h, cur.w, 8);
+  if (gn_conv_out(c, cur, e_nout_w, e_nout_b, cfg_.norm_eps, e_cout_w, e_cout_b, 8, co.p, 8, 0)) {
+    drop(c, cur);
+  } else {
+    Act gn = new_act(c, B, cur.h, cur.w, cur.c);
+    gnorm(c, cur, nullptr, e_nout_w, e_nout_b, cfg_.norm_eps, 1, gn);
+    drop(c, cur);
+    conv2d(c, gn, nullptr, e_cout_w, e_cout_b, 8, 3, 1, 1, 1, gn.h, gn.w, co);
+    drop(c, gn);
+  }
   linear(c, co.p, 8, co.pix(), 8, qw, 8, fptr(qb), moments, 8, ACT_NONE, nullptr, 0, 0, B);
   drop(c, co);
 }
@@ -916,13 +949,17 @@ void Vae::run_decode(Ctx& c, const void* z, int B, int h, int w, void* out) {
       cur = u;
     }
   }
-  Act gn = new_act(c, B, cur.h, cur.w, cur.c);
-  gnorm(c, cur, nullptr, d_nout_w, d_nout_b, cfg_.norm_eps, 1, gn);
-  drop(c, cur);
-  Act o;
-  o.p = out; o.n = B; o.h = gn.h; o.w = gn.w; o.c = 4;
-  conv2d(c, gn, nullptr, d_cout_w, d_cout_b, 4, 3, 1, 1, 1, gn.h, gn.w, o);
-  drop(c, gn);
+  if (gn_conv_out(c, cur, d_nout_w, d_nout_b, cfg_.norm_eps, d_cout_w, d_cout_b, 4, out, 4, 0)) {
+    drop(c, cur);
+  } else {
+    Act gn = new_act(c, B, cur.h, cur.w, cur.c);
+    gnorm(c, cur, nullptr, d_nout_w, d_nout_b, cfg_.norm_eps, 1, gn);
+    drop(c, cur);
+    Act o;
+    o.p = out; o.n = B; o.h = gn.h; o.w = gn.w; o.c = 4;
+    conv2d(c, gn, nullptr, d_cout_w, d_cout_b, 4, 3, 1, 1, 1, gn.h, gn.w, o);
+    drop(c, gn);
+  }
 }
 
 size_t Vae::encode_ws(int B, int H, int W) {

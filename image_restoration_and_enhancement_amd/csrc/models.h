@@ -103,6 +103,8 @@ class Model {
                 Act& out, const float* rowadd = nullptr, long rowadd_ld = 0, const void* residual = nullptr,
                 bool stats = false);
   void lnorm(Ctx& c, const void* x, int rows, int C, P g, P b, float eps, void* out);
+  // GroupNorm + SiLU + 3x3 conv to a narrow output head in one kernel (gn_conv_narrow); false: not taken
+  bool gn_conv_out(Ctx& c, const Act& x, P g, P gb, float eps, P w, P b, int cout, void* out, int ldo, int out_f32);
 
   int kind_;
   irx_model_config cfg_;

@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const double2* _
                                                                 int G, double cnt, float eps,
                                                                 const float* __restrict__ gamma,
                                                                 const float* __restrict__ beta,
-                                                                float2* __restrict__ ab) {
+                                                                float2* __restrict__ ab, float2* __restrict__ mr) {
   __shared__ float2 gmr[8];
   const int n = blockIdx.x, t = threadIdx.x;
   const int C = C0 + C1, cg = C / G;
@@ -254,6 +254,7 @@ __global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const double2* _
     double var = b / cnt - mean * mean;
     if (var < 0.0) var = 0.0;
     gmr[gl] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+    if (mr) mr[(long)n * G + g] = gmr[gl];
   }
   __syncthreads();
   const int c0 = blockIdx.y * 8 * cg, c1 = min(C, c0 + 8 * cg);
@@ -451,7 +452,7 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
     gn_finalize_parts_kernel<<<dim3(N, (G + 7) / 8), 256, 0, s>>>((const double2*)p0, C0, HW / r0,
                                                                   (const double2*)p1, C1, r1 ? HW / r1 : 0, G,
                                                                   (double)HW * ((C0 + C1) / G), eps, gamma, beta,
-                                                                  ab);
+                                                                  ab, nullptr);
     IRX_LAUNCH_CHECK();
   } else {
     gn_stats_t<T>(x0, x1, C0, C1, N, HW, G, eps, gamma, beta, ab, ws, s);
@@ -503,26 +504,38 @@ void ln_t(const void* x, long ldx, int rows, int C, float eps, const float* gamm
   IRX_LAUNCH_CHECK();
 }
 
-// GroupNorm folded into per-image projection weights (gn_fold_weights): one wave per (output row n, image)
+// GroupNorm folded into per-image projection weights (gn_fold_weights): one wave per (output row n, image).
+// GN(x)_k = a_k x_k + b_k with b_k = beta_k - mean_g(k) a_k; the GEMM multiplies x by the STORED o_k = round(W_k a_k),
+// so the bias is formed with those same rounded weights: bias + sum_k (W_k beta_k - o_k mean_g(k)).  The group mean
+// then cancels exactly against the GEMM's sum_k o_k x_k and only the normalised part (x_k - mean) meets the weight
+// rounding — the error of the unfused path, independent of |mean| / std.
 template <typename T>
 __global__ __launch_bounds__(64) void gn_fold_weights_kernel(const T* __restrict__ W, const float* __restrict__ bias,
-                                                             const float2* __restrict__ ab, int N, int K,
+                                                             const float2* __restrict__ ab,
+                                                             const float* __restrict__ beta,
+                                                             const float2* __restrict__ mr, int G, int N, int K,
                                                              T* __restrict__ Wo, float* __restrict__ bo) {
   const int n = blockIdx.x, img = blockIdx.y, lane = threadIdx.x;
+  const int cg = K / G;
   const T* w = W + (long)n * K;
   const float2* a = ab + (long)img * K;
+  const float2* m = mr + (long)img * G;
   T* wo = Wo + ((long)img * N + n) * K;
   float acc = 0.f;
   for (int k0 = lane * 8; k0 < K; k0 += 512) {
     float f[8], o[8];
     Vec16<T>::unpack(*(const uint4*)(w + k0), f);
 #pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f[e] * a[k0 + e].x;
+    const uint4 packed = Vec16<T>::pack(o);
+    *(uint4*)(wo + k0) = packed;
+    Vec16<T>::unpack(packed, o);   // the weights as stored
+#pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float2 v = a[k0 + e];
-      o[e] = f[e] * v.x;
-      acc = fmaf(f[e], v.y, acc);
+      const int k = k0 + e;
+      acc = fmaf(f[e], beta[k], acc);
+      acc = fmaf(-o[e], m[k / cg].x, acc);
     }
-    *(uint4*)(wo + k0) = Vec16<T>::pack(o);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
@@ -531,25 +544,30 @@ __global__ __launch_bounds__(64) void gn_fold_weights_kernel(const T* __restrict
 
 }  // namespace
 
+const float2* gn_mr_ws(const void* ws, int N, int G) {   // (mean, rstd) per (image, group) of the last stats pass
+  return (const float2*)((const char*)ws + (size_t)N * kMaxChunks * G * 2 * sizeof(double));
+}
+
 void group_norm_parts_ab(int C0, int N, int HW, int G, float eps, const float* gamma, const float* beta,
-                         const double* p0, int r0, float2* ab, hipStream_t s) {
+                         const double* p0, int r0, float2* ab, float2* mr, hipStream_t s) {
   IRX_CHECK(G > 0 && G <= 64 && C0 % G == 0 && C0 <= kMaxC, "GroupNorm: channel counts");
   IRX_CHECK(p0 && r0 > 0 && HW % r0 == 0 && ab, "GroupNorm partials missing");
   ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_finalize_parts_kernel") : std::string(), 0.0, s);
   gn_finalize_parts_kernel<<<dim3(N, (G + 7) / 8), 256, 0, s>>>((const double2*)p0, C0, HW / r0, nullptr, 0, 0, G,
-                                                                (double)HW * (C0 / G), eps, gamma, beta, ab);
+                                                                (double)HW * (C0 / G), eps, gamma, beta, ab, mr);
   IRX_LAUNCH_CHECK();
 }
 
-void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* ab, int N, int K, int imgs, void* Wo,
-                     float* bo, hipStream_t s) {
+void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* ab, const float* beta,
+                     const float2* mr, int G, int N, int K, int imgs, void* Wo, float* bo, hipStream_t s) {
   IRX_CHECK(dtype != F32 && K % 8 == 0 && K <= 4096 && N > 0 && imgs > 0, "gn_fold_weights: 16-bit, K % 8 == 0");
+  IRX_CHECK(beta && mr && G > 0 && K % G == 0, "gn_fold_weights: beta and the group means");
   IRX_CHECK(((uintptr_t)W % 16) == 0 && ((uintptr_t)Wo % 16) == 0, "gn_fold_weights: 16-byte aligned rows");
   ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_fold_weights_kernel") : std::string(), 0.0, s);
   if (dtype == F16)
-    gn_fold_weights_kernel<f16_t><<<dim3(N, imgs), 64, 0, s>>>((const f16_t*)W, bias, ab, N, K, (f16_t*)Wo, bo);
+    gn_fold_weights_kernel<f16_t><<<dim3(N, imgs), 64, 0, s>>>((const f16_t*)W, bias, ab, beta, mr, G, N, K, (f16_t*)Wo, bo);
   else
-    gn_fold_weights_kernel<bf16_t><<<dim3(N, imgs), 64, 0, s>>>((const bf16_t*)W, bias, ab, N, K, (bf16_t*)Wo, bo);
+    gn_fold_weights_kernel<bf16_t><<<dim3(N, imgs), 64, 0, s>>>((const bf16_t*)W, bias, ab, beta, mr, G, N, K, (bf16_t*)Wo, bo);
   IRX_LAUNCH_CHECK();
 }
 

@@ -137,6 +137,7 @@ bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can
 bool gemm_gn_fusable(const GemmArgs& a);                  // conv can apply GemmArgs::gn_ab to its operand
 bool gemm_ln_foldable(const GemmArgs& a);                 // large-tile epilogue can apply GemmArgs::ln_rs / ln_u
 bool gemm_emits_ln_parts(const GemmArgs& a);              // large-tile epilogue can emit GemmArgs::ln_out
+int gemm_large_splits(const GemmArgs& a);                 // K splits of the large-tile path (0: not on it)
 bool gemm_bimg_ok(const GemmArgs& a);                     // large-tile path can take per-image B / bias (b_rows)
 extern int g_gn_fold;      // 1: the transformer GroupNorm folded into per-image proj_in weights (0: gn_apply, A/B)
 extern int g_ln_parts;     // 1: transformer producers emit LayerNorm partials, the statistics pass is skipped (0: A/B)
@@ -177,12 +178,22 @@ void group_norm_parts(int dtype, const void* x0, const void* x1, int C0, int C1,
 void group_norm_stats(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
                       const float* gamma, const float* beta, float2* ab, void* ws, hipStream_t s);
 // ... the same scale / shift from producer partials (group_norm_parts' finalize alone; x1 absent)
+// (mr, nullable: (mean, rstd) per (image, group) [N][G])
 void group_norm_parts_ab(int C0, int N, int HW, int G, float eps, const float* gamma, const float* beta,
-                         const double* p0, int r0, float2* ab, hipStream_t s);
+                         const double* p0, int r0, float2* ab, float2* mr, hipStream_t s);
+// GroupNorm(+SiLU) fused into a 3x3 / stride-1 / pad-1 conv to cout <= 16 channels (the models' output heads):
+// out[n][y][x][o] (ldo per pixel, fp32 or the storage type) = bias[o] + conv(act(x * ab.x + ab.y)); x [N][H][W][C]
+bool gn_conv_narrow_ok(int dtype, int C, int cout);
+void gn_conv_narrow(int dtype, const void* x, int N, int H, int W, int C, const float2* ab, int silu, const void* w,
+                    const float* bias, int cout, void* out, int ldo, int out_f32, hipStream_t s);
+extern int g_gn_narrow;   // 1: the output heads take gn_conv_narrow (0: GroupNorm pass + conv, A/B)
+// (mean, rstd) per (image, group) [N][G] left in `ws` by group_norm_stats
+const float2* gn_mr_ws(const void* ws, int N, int G);
 // GroupNorm folded into the projection that consumes it (y = x * a + b per image and channel, then y W^T + bias):
-// Wo[i][n][k] = W[n][k] * ab[i][k].x (rounded to the storage type), bo[i][n] = bias[n] + sum_k W[n][k] * ab[i][k].y
-void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* ab, int N, int K, int imgs, void* Wo,
-                     float* bo, hipStream_t s);
+// Wo[i][n][k] = o = round(W[n][k] * ab[i][k].x) (the storage type), bo[i][n] = bias[n] + sum_k (W[n][k] * beta[k] -
+// o * mean[i][k / (K / G)]) with mr = (mean, rstd) per (image, group): the group mean cancels exactly in the GEMM
+void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* ab, const float* beta,
+                     const float2* mr, int G, int N, int K, int imgs, void* Wo, float* bo, hipStream_t s);
 // gamma / beta may be null: no affine (y = (x - mean) * rstd), the form the folded projections' fallback uses
 void layer_norm(int dtype, const void* x, long ldx, int rows, int C, float eps, const float* gamma,
                 const float* beta, void* out, long ldo, hipStream_t s);
@@ -210,16 +221,12 @@ struct AttnArgs {
   int qrep = 1;           // (set by the launcher) query groups per block over resident K/V
 };
 void attention(const AttnArgs& a, hipStream_t s);
-extern bool g_attn_v2;
-extern int g_attn_v3;    // 32x32x16 kernel for bf16 / fp16 (0: the round-1 kernels, bf16 only)
 extern int g_attn_q2;    // 1: non-causal streamed d = 40 attention with two 32-query groups per wave (attn3q)
 extern int g_attn_pf;    // 1: non-causal streamed d = 40 attention with whole-tile K / V fragment prefetch (attn3 PF)
-extern int g_attn_pipe;  // 1: non-causal streamed d = 40 attention with QK^T one key tile ahead (attn3p)
 extern int g_attn_prio;
 extern int g_attn_qrep;
 extern int g_attn_xcd;   // 1: (batch, head) groups of q-blocks kept on one XCD (K/V shared in its L2)
 extern int g_attn_hm;    // 1: the UNet's q|k|v projections write head-major attention operands
-extern int g_attn_d40;   // bf16: 16x16x32 kernel (irx_set_option("attn_v2", 0) selects the 16x16x16 one)
 
 // ------------------------------------------------------------ elementwise / data movement
 // out[m][f] = h * gelu_erf(g): h = proj[m][f], g = proj[m][F + f]; with interleave64 the proj columns are

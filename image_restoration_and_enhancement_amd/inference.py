@@ -93,9 +93,15 @@ class RestorationPipeline:
         else:
             self.device = device
         engine_cfg = dict((config or {}).get("engine", {}))
-        self.engine_dtype = engine_cfg.get("dtype", "bf16")
+        # fp16 by default: the reference's own GPU dtype (src/inference.py:57), which reproduces the CPU path's
+        # PSNR / SSIM at 3 s.f.; a bf16 UNet runs with an fp16 VAE by default (the bf16 VAE is the stage that moves
+        # SSIM at the third figure: DESIGN.md §5, profiles/r05_parity_stages.txt)
+        self.engine_dtype = engine_cfg.get("dtype", "fp16")
         if self.engine_dtype not in ("bf16", "fp16", "fp32"):
             raise ValueError(f"engine dtype must be 'bf16', 'fp16' or 'fp32', got {self.engine_dtype!r}")
+        self.vae_dtype = engine_cfg.get("vae_dtype", "fp16" if self.engine_dtype == "bf16" else self.engine_dtype)
+        if self.vae_dtype not in ("bf16", "fp16", "fp32"):
+            raise ValueError(f"engine vae_dtype must be 'bf16', 'fp16' or 'fp32', got {self.vae_dtype!r}")
         on_gpu = self.device.startswith("cuda")
         self.dtype = ({"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[self.engine_dtype]
                       if on_gpu else torch.float32)
@@ -144,16 +150,17 @@ class RestorationPipeline:
         from .configs import PipelineConfig
         from .pipelines import SDEngine
         kind = "inpaint" if task == "inpaint" else "img2img"
-        key = (source, kind, self.engine_dtype)
+        key = (source, kind, self.engine_dtype, self.vae_dtype)
         if key not in self._engines:
             if source == "random":
                 pc = PipelineConfig.default(task)
-                eng = SDEngine(pc, self.engine_dtype, self.device, weights="random", weight_seed=0)
+                eng = SDEngine(pc, self.engine_dtype, self.device, weights="random", weight_seed=0,
+                               vae_dtype=self.vae_dtype)
             else:
                 pc = PipelineConfig.from_dir(source, task)
-                eng = SDEngine(pc, self.engine_dtype, self.device, weights=source)
+                eng = SDEngine(pc, self.engine_dtype, self.device, weights=source, vae_dtype=self.vae_dtype)
             self._engines[key] = eng
-            logger.info(f"{task} engine ready ({source}, {self.engine_dtype})")
+            logger.info(f"{task} engine ready ({source}, {self.engine_dtype}, VAE {self.vae_dtype})")
         return NativeSDModel(self._engines[key], kind, source)
 
     def _try_load(self, task: str, train_script: str) -> NativeSDModel:

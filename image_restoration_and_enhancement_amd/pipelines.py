@@ -64,14 +64,19 @@ class SDEngine:
     """The three native models of one task directory + the batched denoising loop."""
 
     def __init__(self, cfg: PipelineConfig, dtype="bf16", device="cuda", weights="random", weight_seed: int = 0,
-                 state_dicts: Optional[Dict[str, Dict[str, torch.Tensor]]] = None):
+                 state_dicts: Optional[Dict[str, Dict[str, torch.Tensor]]] = None, vae_dtype=None, clip_dtype=None):
+        """`dtype` is the UNet's compute type (and the default of the other two models); `vae_dtype` /
+        `clip_dtype` override it per model (e.g. a bf16 UNet with an fp16 VAE)."""
         self.cfg = cfg
         self.dt = dtype_code(dtype)
         self.tdt = TORCH_DT[self.dt]
+        self.vdt = dtype_code(vae_dtype) if vae_dtype is not None else self.dt     # VAE + its pixel / latent I/O
+        self.vtdt = TORCH_DT[self.vdt]
+        self.cdt = dtype_code(clip_dtype) if clip_dtype is not None else self.dt
         self.device = torch.device(device)
         self.unet = UNet(cfg.unet, self.dt, self.device)
-        self.vae = VAE(cfg.vae, self.dt, self.device)
-        self.clip = CLIPText(cfg.clip, self.dt, self.device)
+        self.vae = VAE(cfg.vae, self.vdt, self.device)
+        self.clip = CLIPText(cfg.clip, self.cdt, self.device)
         if state_dicts is None:
             state_dicts = self._load_weights(weights, weight_seed)
         if state_dicts is not None:
@@ -116,7 +121,8 @@ class SDEngine:
         if key not in self._ctx_cache:
             ids = [self.tokenizer(negative), self.tokenizer(prompt)] if cfg_on else [self.tokenizer(prompt)]
             ids = torch.from_numpy(np.stack(ids))
-            self._ctx_cache[key] = self.clip.encode(ids)
+            emb = self.clip.encode(ids)
+            self._ctx_cache[key] = emb if emb.dtype == self.tdt else emb.to(self.tdt)
         return self._ctx_cache[key]
 
     def context_kv(self, emb: torch.Tensor, batch: int) -> torch.Tensor:
@@ -127,27 +133,27 @@ class SDEngine:
     # ------------------------------------------------------------------ building blocks
     def to_tensor(self, u8: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, H, W_, _ = u8.shape
-        out = torch.empty((B, H, W_, 8), dtype=self.tdt, device=self.device)
-        L.call("irx_image_to_tensor", _stream(), self.dt, _p(u8), _p(mask), B, H, W_, 8, _p(out))
+        out = torch.empty((B, H, W_, 8), dtype=self.vtdt, device=self.device)
+        L.call("irx_image_to_tensor", _stream(), self.vdt, _p(u8), _p(mask), B, H, W_, 8, _p(out))
         return out
 
     def sample_latents(self, moments: torch.Tensor, eps: torch.Tensor, noise: Optional[torch.Tensor],
                        a: float = 1.0, b: float = 0.0) -> torch.Tensor:
         B, h, w, _ = moments.shape
         out = torch.empty((B, h, w, 4), dtype=torch.float32, device=self.device)
-        L.call("irx_latent_sample", _stream(), self.dt, _p(moments), B, h, w, _p(eps), _p(noise), 1,
+        L.call("irx_latent_sample", _stream(), self.vdt, _p(moments), B, h, w, _p(eps), _p(noise), 1,
                float(self.cfg.vae.scaling_factor), float(a), float(b), _p(out))
         return out
 
     def decode(self, lat: torch.Tensor, want_float: bool) -> tuple:
         B, h, w, _ = lat.shape
-        z = torch.empty((B, h, w, 8), dtype=self.tdt, device=self.device)
-        L.call("irx_latents_to_vae", _stream(), self.dt, _p(lat), B, h, w, float(self.cfg.vae.scaling_factor), _p(z))
+        z = torch.empty((B, h, w, 8), dtype=self.vtdt, device=self.device)
+        L.call("irx_latents_to_vae", _stream(), self.vdt, _p(lat), B, h, w, float(self.cfg.vae.scaling_factor), _p(z))
         img = self.vae.decode(z)
         H, W_ = h * 8, w * 8
         u8 = torch.empty((B, H, W_, 3), dtype=torch.uint8, device=self.device)
         f01 = torch.empty((B, H, W_, 3), dtype=torch.float32, device=self.device) if want_float else None
-        L.call("irx_tensor_to_image", _stream(), self.dt, _p(img), B, H, W_, 4, _p(u8), _p(f01))
+        L.call("irx_tensor_to_image", _stream(), self.vdt, _p(img), B, H, W_, 4, _p(u8), _p(f01))
         return u8, f01
 
     def _loop_buffers(self, lat: torch.Tensor, plans: List[StepPlan], cfg_on: bool) -> dict:

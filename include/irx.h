@@ -257,6 +257,24 @@ int irx_op_gn_conv3(void* stream, int dtype, const void* x0, const void* x1, int
                     int groups, float eps, const float* gamma, const float* beta, int silu, const void* weight,
                     const float* bias, int cout, const float* rowadd, long rowadd_ld, const void* residual,
                     void* out, void* ws, int* fused);
+/* GroupNorm(+SiLU) -> 3x3 / stride-1 / pad-1 conv to cout <= 16 channels in one kernel: the output heads of the UNet
+   and VAE that src/inference.py:486 runs (conv_norm_out -> conv_out).  x [n][h][w][c] (16-bit, c % 64 == 0),
+   weight [cout][3][3][c], out [n][h][w][ldo] (fp32 when out_f32, else the dtype).  Statistics by a pass over x.
+   ws: irx_op_gn_conv3_ws_bytes(n, h * w, groups, c) bytes. */
+int irx_op_gn_conv_narrow(void* stream, int dtype, const void* x, int n, int h, int w, int c, int groups, float eps,
+                          const float* gamma, const float* beta, int silu, const void* weight, const float* bias,
+                          int cout, void* out, int ldo, int out_f32, void* ws);
+/* GroupNorm (no SiLU) -> projection: the diffusers Transformer2DModel norm -> proj_in of the UNet that
+   src/inference.py:486 runs.  out[i][p][:] = GN(x)[i][p][:] W^T + bias for x [n][hw][k], W [nout][k], out [n][hw][nout].
+   With option gn_fold (default) and a shape whose large-tile row tiles never straddle two images, GroupNorm is folded
+   into per-image weights o = round(W diag(a_i)) and biases bias + W beta - o mean_i (the engine's form; the normalised
+   tensor is never written); otherwise GroupNorm then GEMM.  *folded = 1 when the fold runs, *splits = the large-tile
+   K splits (0: not on the large tiles); query both with out == NULL (nothing launched).
+   ws: irx_op_gn_proj_ws_bytes(n, hw, groups, k, nout) bytes. */
+size_t irx_op_gn_proj_ws_bytes(int n, int hw, int groups, int k, int nout);
+int irx_op_gn_proj(void* stream, int dtype, const void* x, int n, int hw, int k, int groups, float eps,
+                   const float* gamma, const float* beta, const void* w, const float* bias, int nout, void* out,
+                   void* ws, int* folded, int* splits);
 int irx_op_layer_norm(void* stream, int dtype, const void* x, int rows, int c, float eps, const float* gamma,
                       const float* beta, void* out);
 int irx_op_attention(void* stream, int dtype, int batch, int heads, int lq, int lk, int d, const void* q, long ldq,

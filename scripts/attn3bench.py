@@ -44,11 +44,9 @@ def variants(dt, B, Lq, Lk, C):
     def run_hm():
         L.call("irx_op_attention_hm", O.S(), O.DT[dt], B, H, Lq, Lk, d, O.P(hm[0]), O.P(hm[1]), O.P(hm[2]),
                O.P(o), 1.0 / math.sqrt(d))
-    vs = {"v3": (lambda: opt(attn_v3=1, attn_xcd=1), run_il),
-          "v3-hm": (lambda: opt(attn_v3=1, attn_xcd=1), run_hm),
-          "v3-noxcd": (lambda: opt(attn_v3=1, attn_xcd=0), run_il)}
-    if dt == torch.bfloat16:
-        vs["r1"] = (lambda: opt(attn_v3=0, attn_xcd=1), run_il)
+    vs = {"v3": (lambda: opt(attn_xcd=1), run_il),
+          "v3-hm": (lambda: opt(attn_xcd=1), run_hm),
+          "v3-noxcd": (lambda: opt(attn_xcd=0), run_il)}
     return vs
 
 
@@ -76,7 +74,6 @@ for dname in a.dtypes.split(","):
                 e1.record()
                 torch.cuda.synchronize()
                 best[name] = min(best[name], e0.elapsed_time(e1) / a.iters * 1e3)
-        L.call("irx_set_option", b"attn_v3", 1)
         L.call("irx_set_option", b"attn_xcd", 1)
         print(f"{dname} {lab:20s} " + " | ".join(f"{x} {t:8.1f}us {flops / t / 1e6:6.1f}TF"
                                                for x, t in best.items()), flush=True)

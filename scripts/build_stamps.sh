@@ -1,8 +1,9 @@
 #!/bin/bash
-# Timing-diagnostic build of the halo conv (gemm2.hip with -DIRX_HALO_STAMPS: in-kernel s_memtime segment sums in the
+# Timing-diagnostic build of gemm2.hip (-DIRX_HALO_STAMPS: the option gemm_dbg knock-outs of every gemm2 loop, which the
+# product library compiles out, and in-kernel s_memtime segment sums in the
 # HALO == 4 loop, read back by irx_debug_halo_stamps) linked with the regular objects into
 # scripts/_skdbg/libirx_stamps.so (git-ignored and listed in .gpurunignore: drop that line for a stamps run).  Used by
-# scripts/halo_diag.py --stamps.
+# scripts/halo_diag.py --stamps and, with IRX_LIB=scripts/_skdbg/libirx_stamps.so, kbench.py dbg1/dbg2/dbg3.
 set -eu
 cd "$(dirname "$0")/.."
 python3 -m image_restoration_and_enhancement_amd.build > /dev/null

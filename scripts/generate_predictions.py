@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--mode", default="faithful", choices=["faithful", "batched"])
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--random-weights", action="store_true", help="seeded random SD-1.5 weights (smoke runs)")
-    ap.add_argument("--dtype", default=None, help="engine dtype: bf16 (default) | fp16 | fp32")
+    ap.add_argument("--dtype", default=None, help="engine dtype: fp16 (default, the reference GPU dtype) | bf16 | fp32")
     a = ap.parse_args()
     # the driver needs no data collectives (shards are independent; one closing barrier): gloo, so several
     # ranks may also share one GPU

@@ -30,6 +30,10 @@ def _restore_options():
     """Every test leaves the engine's runtime options (irx_set_option) as it found them: a snapshot before the test,
     restored after it (a toggle restored to a non-default value changed what later tests ran)."""
     from image_restoration_and_enhancement_amd import _lib as L
+    try:
+        L.load()          # (loaded before the snapshot: the first test to load the library is restored too, ADVICE r4)
+    except L.IrxError:
+        pass
     before = L.options() if L._lib is not None else None
     yield
     if before is None or L._lib is None:

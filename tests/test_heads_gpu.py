@@ -1,0 +1,121 @@
+"""The models' output heads: GroupNorm -> SiLU -> 3x3 conv to a few channels in one kernel (gn_conv_narrow.hip; the
+UNet's conv_norm_out -> conv_out, the VAE encoder's and decoder's, as diffusers runs them under src/inference.py:486)
+and the UNet input padded to one 64-channel slab in the 16-bit engines (conv_in on the large-tile conv path).
+
+Checked through the C ABI (irx_op_gn_conv_narrow) against PyTorch fp32 GroupNorm + SiLU (rounded to the storage type,
+as the engine's GroupNorm output is) + conv2d with the 16-bit weights, and at the model level: the UNet / VAE with the
+fused heads (option gn_narrow, default) vs the GroupNorm pass + conv path.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from image_restoration_and_enhancement_amd import _lib as L
+from tests import opref as O
+
+pytestmark = pytest.mark.gpu
+
+DT16 = [torch.bfloat16, torch.float16]
+TOL = {torch.bfloat16: 1.5e-2, torch.float16: 3e-3}
+
+
+def _r(*shape, seed=0):
+    return torch.randn(*shape, generator=torch.Generator().manual_seed(seed))
+
+
+def narrow(x, gamma, beta, w, bias, groups, eps, out_f32, ldo, dt, device):
+    n, h, wd, c = x.shape
+    cout = w.shape[0]
+    xd = x.to(dt).to(device).contiguous()
+    wd_ = w.permute(0, 2, 3, 1).to(dt).to(device).contiguous()            # [cout][3][3][c]
+    out = torch.full((n, h, wd, ldo), float("nan"), dtype=torch.float32 if out_f32 else dt, device=device)
+    ws = torch.empty(L.load().irx_op_gn_conv3_ws_bytes(n, h * wd, groups, c), dtype=torch.uint8, device=device)
+    L.call("irx_op_gn_conv_narrow", O.S(), O.DT[dt], O.P(xd), n, h, wd, c, groups, eps, O.P(gamma.to(device)),
+           O.P(beta.to(device)), 1, O.P(wd_), O.P(bias.to(device)), cout, O.P(out), ldo, int(out_f32), O.P(ws))
+    return out
+
+
+def reference(x, gamma, beta, w, bias, groups, eps, dt):
+    xq = x.to(dt).float().permute(0, 3, 1, 2)
+    g = F.silu(F.group_norm(xq, groups, gamma, beta, eps)).to(dt).float()
+    return F.conv2d(g, w.to(dt).float(), bias, padding=1).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("n,h,w,c,cout,out_f32,ldo", [
+    (4, 64, 64, 320, 4, True, 4),      # UNet conv_out (eps prediction, fp32)
+    (2, 32, 32, 512, 8, False, 8),     # VAE encoder conv_out (moments)
+    (1, 96, 80, 128, 3, False, 4),     # VAE decoder conv_out (RGB padded to 4), W not a multiple of 64
+    (3, 7, 5, 320, 4, True, 4),        # odd latent
+])
+def test_gn_conv_narrow_vs_fp32(device, dt, n, h, w, c, cout, out_f32, ldo):
+    x = _r(n, h, w, c, seed=1) * 1.5 + 0.3
+    gamma, beta = 1.0 + 0.2 * _r(c, seed=2), 0.1 * _r(c, seed=3)
+    wt = _r(cout, c, 3, 3, seed=4) / math.sqrt(9 * c)
+    bias = 0.1 * _r(cout, seed=5)
+    got = narrow(x, gamma, beta, wt, bias, 32, 1e-5, out_f32, ldo, dt, device)
+    torch.cuda.synchronize()
+    ref = reference(x, gamma, beta, wt, bias, 32, 1e-5, dt)
+    assert torch.isfinite(got[..., :cout]).all()
+    if ldo > cout:    # padding channels of the output rows are not written
+        assert torch.isnan(got[..., cout:].float()).all()
+    assert O.rel_err(got[..., :cout], ref) < TOL[dt]
+
+
+def test_gn_conv_narrow_refuses_unaligned_channels(device):
+    x = _r(1, 8, 8, 96)
+    with pytest.raises(L.IrxError):
+        narrow(x, torch.ones(96), torch.zeros(96), _r(4, 96, 3, 3), torch.zeros(4), 32, 1e-5, True, 4,
+               torch.bfloat16, device)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_unet_heads_fused_vs_unfused(device, dtype):
+    """UNet at 64x64 latents: the fused output head and the 64-channel conv_in path vs the GroupNorm pass + conv
+    (option gn_narrow 0) — the same arithmetic up to the conv's accumulation order."""
+    from tests import models_common as MC
+    from image_restoration_and_enhancement_amd.engine import UNet
+    pc, sd = MC.state_dicts("denoise")
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    unet = UNet(pc.unet, dtype, device)
+    unet.load_state_dict(sd["unet"])
+    assert unet.cin_pad == 64
+    g = torch.Generator().manual_seed(9)
+    xin = torch.zeros(2, 64, 64, unet.cin_pad)
+    xin[..., :4] = torch.randn(2, 64, 64, 4, generator=g)
+    kv = unet.prepare_context(torch.randn(2, 77, 768, generator=g).to(tdt).to(device).contiguous())
+    outs = []
+    for v in (1, 0):
+        with L.option(gn_narrow=v):
+            outs.append(unet.forward(xin.to(tdt).to(device).contiguous(), torch.full((2,), 481.0, device=device),
+                                     kv, 77).float().cpu())
+    rel = float((outs[0] - outs[1]).norm() / outs[1].norm())
+    print(f"\nUNet heads fused vs unfused ({dtype}): rel L2 {rel:.2e}")
+    assert torch.isfinite(outs[0]).all()
+    assert rel < (2e-3 if dtype == "bf16" else 5e-4), rel
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_vae_heads_fused_vs_unfused(device, dtype):
+    from tests import models_common as MC
+    from image_restoration_and_enhancement_amd.engine import VAE
+    pc, sd = MC.state_dicts("denoise")
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    vae = VAE(pc.vae, dtype, device)
+    vae.load_state_dict(sd["vae"])
+    g = torch.Generator().manual_seed(10)
+    img = torch.zeros(2, 128, 128, 8)
+    img[..., :3] = torch.rand(2, 128, 128, 3, generator=g) * 2 - 1
+    img = img.to(tdt).to(device).contiguous()
+    res = []
+    for v in (1, 0):
+        with L.option(gn_narrow=v):
+            m = vae.encode(img).float().cpu()
+            d = vae.decode(vae.encode(img).contiguous()).float().cpu()
+        res.append((m, d))
+    for k in range(2):
+        rel = float((res[0][k] - res[1][k]).norm() / res[1][k].norm())
+        assert torch.isfinite(res[0][k]).all()
+        assert rel < (1e-2 if dtype == "bf16" else 2e-3), (k, rel)

@@ -559,25 +559,6 @@ def test_attention_d512_flash(device, dt, B, L):
     assert O.rel_err(got, ref) < TOL[dt] * 2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("B,Lq,Lk", [(2, 256, 256), (2, 200, 77), (1, 333, 190)])
-def test_attention_d40_variants(device, variant, B, Lq, Lk):
-    """Every d = 40 bf16 kernel variant (irx_set_option("attn_d40")): 128 / 64-key tiles, ones-column or
-    VALU row sums, d padded to 64 or to 48 with a 16x16x16 tail MFMA."""
-    from image_restoration_and_enhancement_amd import _lib as L
-    dt = torch.bfloat16
-    q, k, v = _r(B, Lq, 320, seed=60), _r(B, Lk, 320, seed=61), _r(B, Lk, 320, seed=62)
-    L.call("irx_set_option", b"attn_d40", variant)
-    L.call("irx_set_option", b"attn_v3", 0)          # the round-1 kernels (attn3 is the default)
-    try:
-        got = O.attention(_dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device), 8)
-    finally:
-        L.call("irx_set_option", b"attn_d40", 2)
-        L.call("irx_set_option", b"attn_v3", 1)
-    ref = O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), 8)
-    assert O.rel_err(got, ref) < 2 * TOL[dt]
-
-
 def test_gemm_splitk_two_streams(device):
     """Two streams running in-kernel split-K GEMMs concurrently (the arrival tickets were one
     process-global array): each stream's results equal a single-stream run bit for bit."""
@@ -706,27 +687,6 @@ def test_gemm_sk_geglu(device, M, dt):
     h, g = pr.chunk(2, dim=-1)
     assert O.rel_err(sk, h * F.gelu(g)) < TOL[dt]
     _same_as_large_tile(sk, _with_sk(0, run), dt)
-
-
-@pytest.mark.parametrize("dt", DT16)
-@pytest.mark.parametrize("B,Lq,Lk", [(2, 1024, 1024), (1, 333, 190), (2, 200, 1000), (1, 64, 129), (2, 4096, 4096)])
-def test_attention_pipelined_d40(device, dt, B, Lq, Lk):
-    """attn3p (option attn_pipe: the QK^T of key tile j+1 issued before tile j's softmax) vs PyTorch fp32 and vs attn3:
-    the same arithmetic except where the deferred max moves (S(j+1) then takes -delta after the MFMA instead of inside
-    it), so the two agree to rounding.  Covers odd tile counts (the key loop is unrolled by two) and ragged key tiles."""
-    from image_restoration_and_enhancement_amd import _lib as L
-    C, heads = 320, 8
-    q, k, v = _r(B, Lq, C, seed=70) * 2, _r(B, Lk, C, seed=71) * 2, _r(B, Lk, C, seed=72)
-    qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
-    with L.option(attn_pipe=1):
-        got = O.attention(qd, kd, vd, heads)
-    with L.option(attn_pipe=0):
-        base = O.attention(qd, kd, vd, heads)
-    torch.cuda.synchronize()
-    assert torch.isfinite(got).all()
-    assert O.rel_err(got, base.float()) < (1e-2 if dt == torch.bfloat16 else 2e-3)
-    ref = O.ref_attention(_q(q[:1], dt), _q(k[:1], dt), _q(v[:1], dt), heads)
-    assert O.rel_err(got[:1], ref) < 2 * TOL[dt]
 
 
 @pytest.mark.parametrize("dt", DT16)

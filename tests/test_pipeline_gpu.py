@@ -58,7 +58,7 @@ def test_model_dir_loading(device, tmp_path):
     assert p.models["denoise"].source == str(root)
     pc, sd = MC.state_dicts("denoise")
     sd16 = {k: {n: t.half().float() for n, t in v.items()} for k, v in sd.items()}
-    eng = SDEngine(pc, "bf16", device, state_dicts=sd16)
+    eng = SDEngine(pc, "bf16", device, state_dicts=sd16, vae_dtype=p.vae_dtype)
     u8 = torch.from_numpy(np.array(img)).to(device)[None].contiguous()
     prompt = p.prompts["denoise"]
     ref = eng.img2img(u8, prompt, 0.3, 20, 5.0, seed=42).images_u8[0].cpu().numpy()

@@ -48,6 +48,12 @@ def test_constructor_attributes():
         INF.RestorationPipeline(device="cpu", config={"engine": {"dtype": "int8"}})
     p3 = INF.RestorationPipeline(device="cpu", config={"engine": {"dtype": "fp16"}})
     assert p3.engine_dtype == "fp16" and p3.dtype == torch.float32      # CPU host: fallbacks only
+    # defaults: fp16 (the reference's GPU dtype, src/inference.py:57); a bf16 UNet gets an fp16 VAE
+    assert INF.RestorationPipeline(device="cpu").engine_dtype == "fp16"
+    p4 = INF.RestorationPipeline(device="cpu", config={"engine": {"dtype": "bf16"}})
+    assert p4.engine_dtype == "bf16" and p4.vae_dtype == "fp16"
+    p5 = INF.RestorationPipeline(device="cpu", config={"engine": {"dtype": "bf16", "vae_dtype": "bf16"}})
+    assert p5.vae_dtype == "bf16"
 
 
 def test_fallbacks_without_gpu(tmp_path, monkeypatch):
