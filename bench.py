@@ -294,6 +294,30 @@ def cpu_baseline_and_parity(eng_bench, sds, device, n_images: int, threads: int)
     return cpu, parity
 
 
+def timed_steps(step, steps: int, warmup: int, device, sync=None) -> tuple:
+    """The bench contract's timed region: `warmup` untimed steps, then exactly `steps` steps bracketed by a barrier and
+    a device synchronisation on both sides; returns (last step's output, the MAX over ranks of the timed seconds)."""
+    sync = sync or torch.cuda.synchronize
+    out = None
+    for _ in range(warmup):
+        out = step()
+    sync()
+    D.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    sync()
+    D.barrier()
+    sync()
+    return out, D.max_over_ranks(time.perf_counter() - t0, device)
+
+
+def throughput(batch: int, world: int, steps: int, elapsed: float) -> tuple:
+    """Whole-job images/s (every rank's `batch` images per step, weak scaling) and ms per step."""
+    return batch * world * steps / elapsed, elapsed / steps * 1e3
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -343,22 +367,10 @@ def main():
             return eng.inpaint(imgs, mask, prompt, spec["strength"], args.sched_steps, spec["guidance"], seed=42)
         return eng.img2img(imgs, prompt, spec["strength"], args.sched_steps, spec["guidance"], seed=42, noise=noise)
 
-    for _ in range(args.warmup):
-        out = step()
-    torch.cuda.synchronize()
-    D.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    D.barrier()
-    torch.cuda.synchronize()
-    el = D.max_over_ranks(time.perf_counter() - t0, device)
+    out, el = timed_steps(step, args.steps, args.warmup, device)
     n_evals = len(out.timesteps)
     finite = bool(torch.isfinite(out.latents).all().item())
-    images = batch * world * args.steps
-    value = images / el
+    value, ms_step = throughput(batch, world, args.steps, el)
     cfg_f = 2 if spec["guidance"] > 1 else 1
     tflop_img = (n_evals * cfg_f * F_UNET[res] + spec["n_enc"] * F_ENC[res] + F_DEC[res]) / 1000.0
 
@@ -406,7 +418,7 @@ def main():
         line = {
             "metric": "restored images/sec @512x512, 50 DDIM steps; PSNR/SSIM vs reference",
             "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 2), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": dtype,
             "data": f"synthetic {res}x{res} {args.task} inputs, seeded random SD-1.5 weights",
             "config": {"workload": f"BASELINE configs[{spec['cfg'] - 1}] {args.task} {res}x{res}, batch {batch}/GPU, "

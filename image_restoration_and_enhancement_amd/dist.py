@@ -71,7 +71,11 @@ def rccl_comm(rank: int, world: int) -> C.c_void_p:
       3. after ncclCommInitRank every rank reports success; if any rank failed, the ranks that did get a
          communicator destroy it and all of them raise.
     The id travels over the torch.distributed rendezvous (host plumbing only — the collectives themselves are
-    RCCL calls inside libirx).  Raises IrxError on every rank, or on none."""
+    RCCL calls inside libirx).  Raises IrxError on every rank, or on none — provided every rank RETURNS from
+    ncclCommInitRank: that call is collective in RCCL (blocking init), so a rank whose init fails partway can leave
+    its peers blocked inside theirs, never reaching step 3.  That case is not recovered here (it would need
+    ncclCommInitRankConfig with blocking = 0, a timeout and ncclCommAbort); the torchrun / driver timeout ends such a
+    job.  (tests/test_dist.py's stubbed init returns immediately and does not model it.)"""
     from . import _lib as L
     if not _all_ok(L.call("irx_rccl_available") == 1):
         raise L.IrxError("librccl cannot be loaded on every rank")

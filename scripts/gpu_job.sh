@@ -15,6 +15,12 @@
 #   py|<name>|<script> <args>           any python script -> <name>.txt
 #   run|<name>|<program> <args>         any program (no shell) -> <name>.txt
 #   sec|<seconds>                       time limit of the following steps (default 600)
+#   torchrun|<name>|<nproc>|<bench.py args>   bench.py on <nproc> GPUs of one node, one rank per GPU over RCCL
+#                                       (python -m torch.distributed.run ... --master-addr 127.0.0.1) -> <name>.json
+#
+# BASELINE.json's multi-GPU configs (the round-end driver runs the 1/2/4/8 scaling itself; these are the same runs):
+#   configs[3] inpaint 512x512, batch 32 over 4 GPUs:  scripts/gpu_job.sh cfg3 "torchrun|inpaint4|4|--task inpaint"
+#   configs[4] colorize 768x768 fp16, batch 64 over 8: scripts/gpu_job.sh cfg4 "torchrun|colorize8|8|--task colorize"
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -64,6 +70,11 @@ for step in "$@"; do
     run)
       timeout -k 10 "$lim" $rest > "$O/$name.txt" 2>&1
       rc=$?; tail -40 "$O/$name.txt"; [ $rc -eq 0 ] || fail "$name" $rc ;;
+    torchrun)
+      IFS='|' read -r np bargs <<< "$rest"
+      timeout -k 10 "$lim" python -m torch.distributed.run --nnodes=1 --nproc-per-node "$np" --master-addr 127.0.0.1 \
+        --master-port "${IRX_MASTER_PORT:-29531}" bench.py --gpus "$np" $bargs > "$O/$name.json" 2> "$O/$name.err"
+      rc=$?; tail -3 "$O/$name.err"; cut -c1-400 "$O/$name.json"; [ $rc -eq 0 ] || fail "$name" $rc ;;
     *) echo "unknown step kind '$kind'"; exit 2 ;;
   esac
 done

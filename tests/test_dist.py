@@ -81,7 +81,9 @@ class _Model:
 
 def _stub_lib(L, rank, scenario, models, log):
     """_lib.call replaced by a stub: the RCCL entry points succeed or fail per `scenario`, and irx_weights_bcast
-    moves the blob with a gloo broadcast so the data path can be checked end to end on the CPU."""
+    moves the blob with a gloo broadcast so the data path can be checked end to end on the CPU.  The stubbed
+    irx_rccl_comm_init returns at once on every rank: it does not model RCCL's blocking (collective) init, where a
+    rank failing partway can leave its peers waiting inside ncclCommInitRank (dist.rccl_comm docstring)."""
     import ctypes as C
     import torch.distributed as dist
     uid = bytes(range(128))

@@ -32,8 +32,11 @@ def narrow(x, gamma, beta, w, bias, groups, eps, out_f32, ldo, dt, device):
     wd_ = w.permute(0, 2, 3, 1).to(dt).to(device).contiguous()            # [cout][3][3][c]
     out = torch.full((n, h, wd, ldo), float("nan"), dtype=torch.float32 if out_f32 else dt, device=device)
     ws = torch.empty(L.load().irx_op_gn_conv3_ws_bytes(n, h * wd, groups, c), dtype=torch.uint8, device=device)
-    L.call("irx_op_gn_conv_narrow", O.S(), O.DT[dt], O.P(xd), n, h, wd, c, groups, eps, O.P(gamma.to(device)),
-           O.P(beta.to(device)), 1, O.P(wd_), O.P(bias.to(device)), cout, O.P(out), ldo, int(out_f32), O.P(ws))
+    # (device copies held in locals until the launch is queued: a temporary's block could be reused by the next copy)
+    gd, bd, bsd = (t.float().to(device).contiguous() for t in (gamma, beta, bias))
+    L.call("irx_op_gn_conv_narrow", O.S(), O.DT[dt], O.P(xd), n, h, wd, c, groups, eps, O.P(gd), O.P(bd), 1, O.P(wd_),
+           O.P(bsd), cout, O.P(out), ldo, int(out_f32), O.P(ws))
+    torch.cuda.synchronize()
     return out
 
 
@@ -109,11 +112,12 @@ def test_vae_heads_fused_vs_unfused(device, dtype):
     img = torch.zeros(2, 128, 128, 8)
     img[..., :3] = torch.rand(2, 128, 128, 3, generator=g) * 2 - 1
     img = img.to(tdt).to(device).contiguous()
+    z = vae.encode(img).contiguous()          # one decoder input for both arms (isolates the decoder's head)
     res = []
     for v in (1, 0):
         with L.option(gn_narrow=v):
             m = vae.encode(img).float().cpu()
-            d = vae.decode(vae.encode(img).contiguous()).float().cpu()
+            d = vae.decode(z).float().cpu()
         res.append((m, d))
     for k in range(2):
         rel = float((res[0][k] - res[1][k]).norm() / res[1][k].norm())
