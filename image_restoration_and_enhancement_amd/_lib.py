@@ -17,6 +17,8 @@ IRX_MODEL_UNET, IRX_MODEL_VAE, IRX_MODEL_CLIP = 0, 1, 2
 IRX_LAYOUT_VEC, IRX_LAYOUT_MAT, IRX_LAYOUT_CONV, IRX_LAYOUT_EMB = 0, 1, 2, 3
 IRX_LAYOUT_MAT_GEGLU64, IRX_LAYOUT_VEC_GEGLU64 = 4, 5
 IRX_LAYOUT_VEC_LN_U, IRX_LAYOUT_VEC_LN_V = 6, 7
+IRX_LAYOUT_MAT_CHAIN, IRX_LAYOUT_VEC_CHAIN = 8, 9
+IRX_LAYOUT_CONV_UP2 = 10
 IRX_RCCL_ID_BYTES = 128   # include/irx.h (sizeof(ncclUniqueId))
 
 

@@ -71,6 +71,9 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gn_v2", nullptr, &g_gn_v2},
     {"gn_fuse", &g_gn_fuse, nullptr},
     {"gn_parts", &g_gn_parts, nullptr},
+    {"gn_red_parts", &g_gn_red_parts, nullptr},
+    {"ff_chain", &g_ff_chain, nullptr},
+    {"up2", &g_up2, nullptr},
     {"ln_parts", &g_ln_parts, nullptr},
     {"gn_fold", &g_gn_fold, nullptr},
     {"gn_narrow", &g_gn_narrow, nullptr},

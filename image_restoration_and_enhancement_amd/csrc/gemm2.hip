@@ -1161,7 +1161,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
             A += v.x;
             B += v.y;
           }
-          *(double2*)(a.gn_part + ((long)(m0 / BM) * a.N + n0 + col) * 2) = make_double2(A, B);
+          long rb = m0 / BM;
+          if (a.up2_w) {   // sub-pixel output: this parity's blocks of an image sit among the image's 4 x rpl
+            const long rpl = (long)a.up2_h * a.up2_w / BM;
+            rb = (rb / rpl * 4 + a.up2_p) * rpl + rb % rpl;
+          }
+          *(double2*)(a.gn_part + (rb * a.N + n0 + col) * 2) = make_double2(A, B);
         }
         return;
       }
@@ -1323,6 +1328,74 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
   }
 }
 
+// The same reduce + epilogue for a 16-bit output that feeds a GroupNorm (GemmArgs::gn_part), also emitting the
+// GroupNorm partials of the stored values per block of kRedGnRows rows (the 8x8-level convs: 64 rows = one image),
+// so no statistics pass over the tensor follows.  Block = kRedGnRows rows x 64 channels: thread = one 16-byte
+// channel chunk (8 of them) x a row stride of 32; shifted fp32 sums of the rounded outputs -> raw fp64, folded over
+// the 32 row lanes through LDS in a fixed order (the large-tile epilogue's arithmetic; batch invariant: a row block
+// never straddles two images).
+constexpr int kRedGnRows = 64;
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_gn_kernel(GemmArgs a, const float* __restrict__ ws, int splits,
+                                                               int Mp, int Np) {
+  __shared__ double2 red[32][64];
+  const int cc = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int m0 = blockIdx.x * kRedGnRows, n = blockIdx.y * 64 + cc * 8;
+  float x0[8], sm[8], sq[8];
+  int cnt = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { x0[e] = 0.f; sm[e] = 0.f; sq[e] = 0.f; }
+  for (int r = rl; r < kRedGnRows; r += 32) {
+    const int m = m0 + r;
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = 0.f;
+    for (int s2 = 0; s2 < splits; ++s2) {
+      const float4* p = (const float4*)(ws + ((long)s2 * Mp + m) * Np + n);
+      const float4 x = p[0], y = p[1];
+      f[0] += x.x; f[1] += x.y; f[2] += x.z; f[3] += x.w; f[4] += y.x; f[5] += y.y; f[6] += y.z; f[7] += y.w;
+    }
+    float rv[8];
+    if (a.residual) Vec16<T>::unpack(*(const uint4*)((const uint16_t*)a.residual + (long)m * a.ldr + n), rv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = f[e] * a.alpha + (a.bias ? a.bias[n + e] : 0.f);
+      if (a.rowadd) v += a.rowadd[(long)(m / a.rows_per_group) * a.rowadd_ld + n + e];
+      v = apply_act(v, a.act);
+      if (a.residual) v += rv[e];
+      f[e] = v * a.out_scale;
+    }
+    const uint4 u = Vec16<T>::pack(f);
+    *(uint4*)((uint16_t*)a.C + (long)m * a.ldc + n) = u;
+    Vec16<T>::unpack(u, f);                           // the stored (rounded) values
+    if (cnt == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x0[e] = f[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float dv = f[e] - x0[e];
+      sm[e] += dv;
+      sq[e] = fmaf(dv, dv, sq[e]);
+    }
+    ++cnt;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const double x = x0[e], sd = sm[e];
+    red[rl][cc * 8 + e] = make_double2(cnt * x + sd, cnt * x * x + 2.0 * x * sd + (double)sq[e]);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    double A = 0.0, B = 0.0;
+    for (int g = 0; g < 32; ++g) {
+      A += red[g][threadIdx.x].x;
+      B += red[g][threadIdx.x].y;
+    }
+    *(double2*)(a.gn_part + ((long)blockIdx.x * a.N + blockIdx.y * 64 + threadIdx.x) * 2) = make_double2(A, B);
+  }
+}
+
 template <typename T, int BM, int BN, int WM, int WN, int BK, int S, int HALO, bool PP>
 void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -1352,7 +1425,13 @@ void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
     }
     IRX_LAUNCH_CHECK();
   }
-  if (sp.splits > 1 && !sp.inkernel) {
+  if (sp.splits > 1 && !sp.inkernel && a.gn_part) {   // (host: gemm_emits_gn_parts checked the shape)
+    ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::splitk_reduce_gn_kernel<") + tn + ">"
+                           : std::string(),
+                 0.0, s);
+    splitk_reduce_gn_kernel<T><<<dim3(a.M / kRedGnRows, a.N / 64), 256, 0, s>>>(a, sp.ws, sp.splits, sp.Mp, sp.Np);
+    IRX_LAUNCH_CHECK();
+  } else if (sp.splits > 1 && !sp.inkernel) {
     ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::splitk_reduce_kernel<") + tn + ", " +
                                  (a.out_f32 ? "true" : "false") + ">"
                            : std::string(),
@@ -1526,18 +1605,29 @@ bool gemm_gn_fusable(const GemmArgs& a) {
 }
 
 int g_gn_parts = 1;
+int g_gn_red_parts = 1;   // irx_set_option("gn_red_parts", 0): split-K reduce kernels do not emit GroupNorm partials (A/B)
 
 int gemm_emits_gn_parts(const GemmArgs& a) {
   if (!g_gn_parts || !g_large_tiles || !is16(a.dtype) || !eligible(a) || !vec_ok(a)) return 0;
   if (a.geglu || a.hs_L || a.batch != 1 || a.out_f32) return 0;
   if (halo_bn(a)) return a.M % 256 == 0 ? 256 : 0;
   const Choice c = choose(a);
-  if (c.BM == 0 || a.M % c.BM) return 0;
-  if (c.splits > 1) {   // the in-kernel split-K reduction runs the epilogue; the separate reduce kernel does not
+  if (c.BM == 0) return 0;
+  if (c.splits > 1) {   // the in-kernel split-K reduction runs the epilogue; the separate reduce kernel emits them too
     const long tiles = (long)((a.M + c.BM - 1) / c.BM) * ((a.N + c.BN - 1) / c.BN);
-    if (!(g_splitk_inkernel && c.splits == 2 && tiles <= kSplitCounters)) return 0;
+    if (!(g_splitk_inkernel && c.splits == 2 && tiles <= kSplitCounters))   // splitk_reduce_gn_kernel
+      return (g_gn_red_parts && !a.up2_w && !c.small && c.BM != 64 && a.M % kRedGnRows == 0 && a.N % 64 == 0 && a.act == ACT_NONE)
+                 ? kRedGnRows : 0;
   }
-  return c.BM;
+  if (a.up2_w && ((long)a.up2_h * a.up2_w) % c.BM) return 0;   // (a sub-pixel tile's rows in one image)
+  return a.M % c.BM ? 0 : c.BM;
+}
+
+bool gemm_up2_ok(const GemmArgs& a) {
+  // every store of the large-tile path goes through c_off (the 16-byte epilogue, the split-K reduce kernel); the
+  // scalar epilogue and the 4-wave kernel do not map rows
+  return g_large_tiles && eligible(a) && vec_ok(a) && !halo_bn(a) && !gemm_sk_eligible(a) && a.batch == 1 &&
+         !a.hs_L && choose(a).BM != 0;
 }
 
 int g_ln_fold = 1;

@@ -24,6 +24,8 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ---------------------------------------------------------------------------------------------- Arena
 int g_arena_guard = 0;
+int g_ff_chain = 1;
+int g_up2 = 1;
 constexpr size_t kGuard = 64 * 1024;
 
 void* Arena::alloc(size_t bytes) {
@@ -237,6 +239,50 @@ bool Model::gn_conv_out(Ctx& c, const Act& x, P g, P gb, float eps, P w, P b, in
   return true;
 }
 
+P Model::up2_weights(const std::string& name, int ch) {
+  if (dt_ == F32) return P();   // (the fp32 parity engine keeps the resize conv: operation for operation the oracle)
+  return reg(name, IRX_LAYOUT_CONV_UP2, dt_, {4 * ch, 2, 2, ch});
+}
+
+void Model::upsample_conv(Ctx& c, const Act& x, P w, P w2, P b, int cout, Act& out, bool stats) {
+  // output pixel (2y + a, 2x + b) of nearest-2x + conv3x3 only sees low-resolution rows y - 1 + a .. y + a and columns
+  // x - 1 + b .. x + b: parity p = 2a + b is a 2x2 conv of x with pad (1 - a, 1 - b) (include/irx.h
+  // IRX_LAYOUT_CONV_UP2), stored at the strided high-resolution pixels (GemmArgs::up2_*): 4 / 9 of the MACs
+  Act lo = out;
+  lo.h = x.h; lo.w = x.w;
+  GemmArgs a = conv_args(dt_, x, nullptr, w2.set ? ptr(w2) : nullptr, b.set ? fptr(b) : nullptr, cout, 2, 1, 1, 1, x.h,
+                         x.w, lo, nullptr, 0, nullptr, 0, -1);
+  a.up2_h = x.h; a.up2_w = x.w;
+  if (!(w2.set && g_up2 && out.h == 2 * x.h && out.w == 2 * x.w && x.c == cout && gemm_up2_ok(a))) {
+    conv2d(c, x, nullptr, w, b, cout, 3, 1, 1, 1, out.h, out.w, out, nullptr, 0, nullptr, 0, -1, stats);
+    return;
+  }
+  if (stats && !out.gnp) {
+    const int r = gemm_emits_gn_parts(a);
+    if (r > 0 && ((long)x.h * x.w) % r == 0) {
+      out.gnp = (double*)c.ws->alloc((size_t)(4L * a.M / r) * cout * 2 * sizeof(double));
+      out.gnr = r;
+    }
+  }
+  const size_t wsb = gemm_workspace_bytes(a);
+  void* p = wsb ? c.ws->alloc(wsb) : nullptr;
+  if (!c.ws->dry()) {
+    const size_t per = (size_t)cout * 4 * x.c * dsize(dt_);   // one parity's [Cout][2][2][Cin]
+    for (int par = 0; par < 4; ++par) {
+      GemmArgs q = a;
+      q.g.pad_t = 1 - (par >> 1);
+      q.g.pad_l = 1 - (par & 1);
+      q.B = (const char*)ptr(w2) + par * per;
+      q.up2_p = par;
+      q.gn_part = out.gnp;
+      q.splitk_ws = p;
+      q.splitk_ws_bytes = wsb;
+      gemm(q, c.s);
+    }
+  }
+  if (p) c.ws->free(p);
+}
+
 void Model::lnorm(Ctx& c, const void* x, int rows, int C, P g, P b, float eps, void* out) {
   if (c.ws->dry()) return;
   layer_norm(dt_, x, C, rows, C, eps, fptr(g), fptr(b), out, C, c.s);
@@ -308,6 +354,11 @@ Unet::XfW Unet::make_xf(const std::string& p, int c) {
   }
   a.ff2w = mat(b + "ff.net.2.weight", c, 4 * c); a.ff2b = vec(b + "ff.net.2.bias", c);
   a.pow = mat(p + "proj_out.weight", c, c); a.pob = vec(p + "proj_out.bias", c);
+  if (dt_ != F32) {   // (the fp32 parity engine keeps the two layers: operation for operation the oracle)
+    const std::string ch = p + "proj_out.weight|" + b + "ff.net.2.weight";
+    a.pofw = reg(ch, IRX_LAYOUT_MAT_CHAIN, dt_, {c, 5 * c});
+    a.pofb = reg(ch, IRX_LAYOUT_VEC_CHAIN, F32, {c}, 1.f, 0, p + "proj_out.bias;" + b + "ff.net.2.bias");
+  }
   return a;
 }
 
@@ -368,6 +419,7 @@ Unet::Unet(const irx_model_config& cfg, int dtype) : Model(IRX_MODEL_UNET, cfg, 
     if (blk.resample) {
       const std::string p = "up_blocks." + std::to_string(i) + ".upsamplers.0.conv.";
       blk.rsw = conv(p + "weight", out_ch, 3, 3, out_ch); blk.rsb = vec(p + "bias", out_ch);
+      blk.rsw2 = up2_weights(p + "weight", out_ch);
     }
     up_.push_back(blk);
   }
@@ -571,6 +623,23 @@ Act Unet::transformer(Ctx& c, const XfW& a, Act& x, const void* kv, int L) {
       c.ws->free(ff);
     }
   }
+  if (a.pofw.set && g_ff_chain) {
+    // ff.net.2 -> (+ h) -> proj_out (+ x) as ONE GEMM: nothing non-linear sits between the two layers, so
+    //   proj_out(h + ff2(g)) + x = [W_po | W_po W_ff2] [h; g] + (b_po + W_po b_ff2) + x
+    // a 1x1 conv over the channel concat (h | g) (K = 5C): the ff2 output is neither written nor re-read and one
+    // launch goes (include/irx.h IRX_LAYOUT_MAT_CHAIN)
+    if (st) c.ws->free(st);
+    c.ws->free(att);
+    c.ws->free(n);
+    if (lnp) c.ws->free(lnp);
+    Act ga;
+    ga.p = g; ga.n = B; ga.h = x.h; ga.w = x.w; ga.c = 4 * C;
+    Act out = new_act(c, B, x.h, x.w, C);
+    conv2d(c, h, &ga, a.pofw, a.pofb, C, 1, 1, 0, 0, x.h, x.w, out, nullptr, 0, x.p, 0, -1, true);
+    c.ws->free(g);
+    drop(c, h);
+    return out;
+  }
   linear(c, g, 4 * C, M, 4 * C, a.ff2w, C, fptr(a.ff2b), h.p, C, ACT_NONE, h.p, C, 0, B);
   c.ws->free(g);
   if (st) c.ws->free(st);
@@ -653,7 +722,7 @@ void Unet::run(Ctx& c, const void* x, int B, int h, int w, const float* t, const
       // Upsample2D: nearest resize to the next skip's size (== 2x unless a latent side is not /8)
       const int th = skips.back().h, tw = skips.back().w;
       Act u = new_act(c, B, th, tw, blk.ch);
-      conv2d(c, cur, nullptr, blk.rsw, blk.rsb, blk.ch, 3, 1, 1, 1, th, tw, u, nullptr, 0, nullptr, 0, -1, true);
+      upsample_conv(c, cur, blk.rsw, blk.rsw2, blk.rsb, blk.ch, u, true);
       drop(c, cur);
       cur = u;
     }
@@ -769,6 +838,7 @@ Vae::Vae(const irx_model_config& cfg, int dtype) : Model(IRX_MODEL_VAE, cfg, dty
       const std::string p = "decoder.up_blocks." + std::to_string(i) + ".upsamplers.0.conv.";
       d_up_w_.push_back(conv(p + "weight", out_ch, 3, 3, out_ch));
       d_up_b_.push_back(vec(p + "bias", out_ch));
+      d_up2_w_.push_back(up2_weights(p + "weight", out_ch));
     }
   }
   d_nout_w = vec("decoder.conv_norm_out.weight", bo[0]); d_nout_b = vec("decoder.conv_norm_out.bias", bo[0]);
@@ -943,8 +1013,7 @@ void Vae::run_decode(Ctx& c, const void* z, int B, int h, int w, void* out) {
     }
     if (i < nb - 1) {
       Act u = new_act(c, B, cur.h * 2, cur.w * 2, cur.c);
-      conv2d(c, cur, nullptr, d_up_w_[i], d_up_b_[i], cur.c, 3, 1, 1, 1, cur.h * 2, cur.w * 2, u, nullptr, 0, nullptr, 0,
-             -1, true);
+      upsample_conv(c, cur, d_up_w_[i], d_up2_w_[i], d_up_b_[i], cur.c, u, true);
       drop(c, cur);
       cur = u;
     }

@@ -103,6 +103,10 @@ class Model {
                 Act& out, const float* rowadd = nullptr, long rowadd_ld = 0, const void* residual = nullptr,
                 bool stats = false);
   void lnorm(Ctx& c, const void* x, int rows, int C, P g, P b, float eps, void* out);
+  // diffusers Upsample2D (nearest resize to out's size, conv 3x3 pad 1): as 4 per-parity 2x2 convs of x (w2:
+  // IRX_LAYOUT_CONV_UP2) when out is exactly 2x and the large-tile path takes the shape, else the resize conv (w)
+  void upsample_conv(Ctx& c, const Act& x, P w, P w2, P b, int cout, Act& out, bool stats);
+  P up2_weights(const std::string& name, int ch);   // IRX_LAYOUT_CONV_UP2 entry (16-bit engines; unset for fp32)
   // GroupNorm + SiLU + 3x3 conv to a narrow output head in one kernel (gn_conv_narrow); false: not taken
   bool gn_conv_out(Ctx& c, const Act& x, P g, P gb, float eps, P w, P b, int cout, void* out, int ldo, int out_f32);
 
@@ -139,6 +143,8 @@ class Unet : public Model {
     // LayerNorm fold (16-bit engines, ln_fold_): qkvw / q2w / ffw hold W * gamma; u = row sums of those, v = bias +
     // W beta (GemmArgs::ln_rs / ln_u)
     P qkvu, qkvv, q2u, q2v, ffu, ffv;
+    // ff.net.2 folded through proj_out (16-bit engines): [W_po | W_po W_ff2] and b_po + W_po b_ff2 (IRX_LAYOUT_*_CHAIN)
+    P pofw, pofb;
     int c = 0;
     long kv_off = 0;      // column offset into the fused cross-attention K|V cache
   };
@@ -147,6 +153,7 @@ class Unet : public Model {
     std::vector<XfW> attn;
     bool has_attn = false, resample = false;
     P rsw, rsb;           // down/upsampler conv
+    P rsw2;               // upsampler: per-parity 2x2 weights (IRX_LAYOUT_CONV_UP2; 16-bit engines)
     int ch = 0;
   };
   ResW make_res(const std::string& p, int cin, int cout);
@@ -195,7 +202,7 @@ class Vae : public Model {
   P e_cin_w, e_cin_b, e_nout_w, e_nout_b, e_cout_w, e_cout_b, qw, qb, pqw, pqb, d_cin_w, d_cin_b, d_nout_w,
       d_nout_b, d_cout_w, d_cout_b;
   std::vector<std::vector<ResW>> e_res_, d_res_;
-  std::vector<P> e_down_w_, e_down_b_, d_up_w_, d_up_b_;
+  std::vector<P> e_down_w_, e_down_b_, d_up_w_, d_up_b_, d_up2_w_;
   ResW e_mid0_, e_mid1_, d_mid0_, d_mid1_;
   AttW e_att_, d_att_;
 };

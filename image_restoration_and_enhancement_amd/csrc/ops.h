@@ -75,6 +75,11 @@ struct GemmArgs {
   // multiplied by B + i * b_img_stride and get bias + i * bias_img_stride (0: one B / bias for every row; a tile never
   // straddles two images: gemm_bimg_ok)
   int b_rows = 0; long b_img_stride = 0; long bias_img_stride = 0;
+  // sub-pixel output (a nearest-2x upsampler's conv as 4 per-parity 2x2 convs, IRX_LAYOUT_CONV_UP2): the GEMM's row m
+  // is low-resolution pixel (image, y, x) of an up2_h x up2_w image and is stored at high-resolution pixel
+  // (image, 2y + a, 2x + b), parity up2_p = 2a + b (0: off).  GroupNorm partials go to row block
+  // (image * 4 + up2_p) * (up2_h * up2_w / BM) + the block within the image (per image contiguous).
+  int up2_h = 0, up2_w = 0, up2_p = 0;
   void* splitk_ws = nullptr; size_t splitk_ws_bytes = 0;   // caller workspace for split-K partials
   // (set by the launcher) N-major tile order: consecutive tiles (one XCD's range) share a B panel instead of an A
   // panel — for the weight-heavy small-M shapes (8x8-level convs: 29.5 MB of weights for 1024 rows)
@@ -119,13 +124,17 @@ __device__ __forceinline__ float2 ln_rs_at(const float2* __restrict__ rs, const 
 }
 // element offset of output (m, n) in C (see GemmArgs::hs_L).  Fields passed by value: a reference to the
 // kernel-argument struct would make the compiler copy all of it to scratch.
-__host__ __device__ __forceinline__ long c_off_f(long m, int n, long ldc, int M, int hs_L, int hs_C, int hs_d) {
+__host__ __device__ __forceinline__ long c_off_f(long m, int n, long ldc, int M, int hs_L, int hs_C, int hs_d, int up2_w,
+                                                 int up2_p) {
+  // (sub-pixel: (image * 2H + 2y + a) * 2W + 2x + b = 2 (m + W floor(m / W)) + 2 W a + b)
+  if (up2_w) return (2 * (m + (long)up2_w * (m / up2_w)) + 2L * up2_w * (up2_p >> 1) + (up2_p & 1)) * ldc + n;
   if (hs_L == 0) return m * ldc + n;
   const int part = n / hs_C, rem = n - part * hs_C, hd = rem / hs_d, e = rem - hd * hs_d;
   const long img = m / hs_L, tok = m - img * hs_L;
   return (long)part * M * hs_C + ((img * (hs_C / hs_d) + hd) * hs_L + tok) * hs_d + e;
 }
-#define c_off(a, m, n) c_off_f((m), (n), (a).ldc, (a).M, (a).hs_L, (a).hs_C, (a).hs_d)
+#define c_off(a, m, n) c_off_f((m), (n), (a).ldc, (a).M, (a).hs_L, (a).hs_C, (a).hs_d, (a).up2_w, (a).up2_p)
+bool gemm_up2_ok(const GemmArgs& a);   // the large-tile path can store a sub-pixel (GemmArgs::up2_*) output
 void gemm(const GemmArgs& a, hipStream_t s);
 bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path; false if not eligible
 bool gemm_sk(const GemmArgs& a, hipStream_t s);           // K = 320 streaming path (gemm_sk.hip); false if not eligible
@@ -137,6 +146,9 @@ bool gemm_geglu_fusable(const GemmArgs& a);               // large-tile path can
 bool gemm_gn_fusable(const GemmArgs& a);                  // conv can apply GemmArgs::gn_ab to its operand
 bool gemm_ln_foldable(const GemmArgs& a);                 // large-tile epilogue can apply GemmArgs::ln_rs / ln_u
 bool gemm_emits_ln_parts(const GemmArgs& a);              // large-tile epilogue can emit GemmArgs::ln_out
+extern int g_up2;            // 1: nearest-2x upsampler convs as 4 per-parity 2x2 convs (IRX_LAYOUT_CONV_UP2; 0: A/B)
+extern int g_ff_chain;       // 1: 16-bit UNets run ff.net.2 -> proj_out as one GEMM (IRX_LAYOUT_MAT_CHAIN; 0: two, A/B)
+extern int g_gn_red_parts;   // 1: split-K reduce kernels emit GroupNorm partials (per 64-row block)
 int gemm_large_splits(const GemmArgs& a);                 // K splits of the large-tile path (0: not on it)
 bool gemm_bimg_ok(const GemmArgs& a);                     // large-tile path can take per-image B / bias (b_rows)
 extern int g_gn_fold;      // 1: the transformer GroupNorm folded into per-image proj_in weights (0: gn_apply, A/B)

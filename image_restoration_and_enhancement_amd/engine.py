@@ -105,6 +105,23 @@ def _convert(t: torch.Tensor, layout: int) -> torch.Tensor:
     return t
 
 
+UP2_TAPS = {(0, 0): (0,), (0, 1): (1, 2), (1, 0): (0, 1), (1, 1): (2,)}   # R(a, i): include/irx.h IRX_LAYOUT_CONV_UP2
+
+
+def conv_up2(w: torch.Tensor) -> torch.Tensor:
+    """OIHW 3x3 weights of a nearest-2x upsampler's conv -> [4 Cout, 2, 2, Cin] per-parity 2x2 weights (fp64 sums)."""
+    w = w.double()
+    out = torch.zeros(4, w.shape[0], 2, 2, w.shape[1], dtype=torch.float64)
+    for a in range(2):
+        for b in range(2):
+            for i in range(2):
+                for j in range(2):
+                    for ky in UP2_TAPS[(a, i)]:
+                        for kx in UP2_TAPS[(b, j)]:
+                            out[2 * a + b, :, i, j, :] += w[:, :, ky, kx]
+    return out.reshape(4 * w.shape[0], 2, 2, w.shape[1])
+
+
 def _pad_to(t: torch.Tensor, shape: Tuple[int, ...]) -> torch.Tensor:
     if tuple(t.shape) == tuple(shape):
         return t
@@ -174,8 +191,21 @@ class NativeModel:
                 t[:p.scale_rows] *= p.row_scale
             return t
 
+        def chain(p: ParamSpec):                       # (A [N][C], B [C][K]) of a MAT_CHAIN / VEC_CHAIN entry
+            a, b = p.name.split("|")
+            return sd[a].double().reshape(sd[a].shape[0], -1), sd[b].double().reshape(sd[b].shape[0], -1)
+
         for p in self.manifest():
-            if p.layout == L.IRX_LAYOUT_VEC_LN_U:
+            if p.layout == L.IRX_LAYOUT_CONV_UP2:        # per-parity 2x2 weights of an upsampler (include/irx.h)
+                t = conv_up2(sd[p.name]).float()
+            elif p.layout == L.IRX_LAYOUT_MAT_CHAIN:     # [A | A B] (include/irx.h)
+                A, Bm = chain(p)
+                t = torch.cat([A, A @ Bm], dim=1).float()
+            elif p.layout == L.IRX_LAYOUT_VEC_CHAIN:     # a + A b
+                A, _ = chain(p)
+                an, bn = p.aux.split(";")
+                t = (sd[an].double().reshape(-1) + A @ sd[bn].double().reshape(-1)).float()
+            elif p.layout == L.IRX_LAYOUT_VEC_LN_U:
                 _, _, wq = mats[p.name]
                 t = wq.double().sum(dim=1).float()
             elif p.layout == L.IRX_LAYOUT_VEC_LN_V:

@@ -48,6 +48,20 @@ extern "C" {
  *             aux = "<beta name>;<bias spec or empty>" */
 #define IRX_LAYOUT_VEC_LN_U 6
 #define IRX_LAYOUT_VEC_LN_V 7
+/* Two linear layers with nothing between them folded into one (16-bit UNets: a Transformer2DModel's ff.net.2 ->
+ * proj_out, the residual add between them distributing over proj_out): name "<A>|<B>" with A [N][C] the second
+ * layer (proj_out.weight) and B [C][K] the first (ff.net.2.weight):
+ *   MAT_CHAIN  [N][C + K] = [A | A B]   (product in fp64, then the cast): proj_out(h + ff2(g)) = [A | AB] [h; g] + ...
+ *   VEC_CHAIN  [N] = a + A b, aux = "<a name>;<b name>" (the biases: proj_out.bias; ff.net.2.bias) */
+#define IRX_LAYOUT_MAT_CHAIN 8
+#define IRX_LAYOUT_VEC_CHAIN 9
+/* A nearest-2x upsampler's 3x3 conv (diffusers Upsample2D: interpolate(scale 2, nearest) -> conv 3x3 pad 1) folded per
+ * output parity (16-bit engines): output pixel (2y + a, 2x + b) only sees low-resolution rows y - 1 + a .. y + a and
+ * columns x - 1 + b .. x + b, so each parity p = 2a + b is a 2x2 conv of the low-resolution input.  [4][Cout][2][2][Cin]
+ * (as [4 Cout][2][2][Cin]) from OIHW: tap (i, j) of parity (a, b) = sum of the original taps ky in R(a, i), kx in
+ * R(b, j), R(0, 0) = {0}, R(0, 1) = {1, 2}, R(1, 0) = {0, 1}, R(1, 1) = {2} (sums in fp64, then the cast).  4 / 9 of
+ * the upsampled conv's MACs. */
+#define IRX_LAYOUT_CONV_UP2 10
 
 typedef struct irx_model irx_model;
 

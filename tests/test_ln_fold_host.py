@@ -80,6 +80,37 @@ def test_ln_fold_option_off_packs_plain(monkeypatch):
     L.call("irx_set_option", b"ln_fold", 0)
     try:
         m = UNet(_small_cfg(), "bf16", "cpu")
-        assert not any(p.aux for p in m.manifest())
+        assert not any(p.aux and p.layout != L.IRX_LAYOUT_VEC_CHAIN for p in m.manifest())
     finally:
         L.call("irx_set_option", b"ln_fold", 1)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_ff2_proj_out_chain_identity(dtype):
+    """IRX_LAYOUT_MAT_CHAIN / VEC_CHAIN (include/irx.h): one GEMM over the concat (h | g) equals diffusers'
+    proj_out(h + ff.net.2(g)) — the transformer's last two layers with the residual add between them."""
+    cfg = _small_cfg()
+    m = UNet(cfg, dtype, "cpu")
+    sd = W.random_state_dict("unet", cfg, 5)
+    e = _entries(m, m.pack(sd))
+    chains = [k for k in e if k[1] == L.IRX_LAYOUT_MAT_CHAIN]
+    assert len(chains) == 4                      # one per transformer (down, mid, 2 up)
+    g = torch.Generator().manual_seed(1)
+    for name, _ in chains:
+        wc = e[(name, L.IRX_LAYOUT_MAT_CHAIN)][1].double()
+        pb, bc = e[(name, L.IRX_LAYOUT_VEC_CHAIN)]
+        po, ff2 = name.split("|")
+        C = sd[po].shape[0]
+        wpo, wff2 = sd[po].double().reshape(C, -1), sd[ff2].double().reshape(C, -1)
+        a_name, b_name = pb.aux.split(";")
+        h = torch.randn(9, C, generator=g, dtype=torch.float64)
+        gg = torch.randn(9, 4 * C, generator=g, dtype=torch.float64)
+        ref = (h + gg @ wff2.T + sd[b_name].double()) @ wpo.T + sd[a_name].double()
+        got = torch.cat([h, gg], 1) @ wc.T + bc.double()
+        tol = 2e-2 if dtype == "bf16" else 3e-3    # the 16-bit rounding of [W_po | W_po W_ff2]
+        assert float((got - ref).norm() / ref.norm()) < tol, name
+
+
+def test_fp32_engine_packs_no_chain():
+    m = UNet(_small_cfg(), "fp32", "cpu")
+    assert not any(p.layout in (L.IRX_LAYOUT_MAT_CHAIN, L.IRX_LAYOUT_VEC_CHAIN) for p in m.manifest())
