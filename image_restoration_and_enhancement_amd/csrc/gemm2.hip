@@ -1483,8 +1483,7 @@ Choice choose(const GemmArgs& a) {
     const int BM = g_gemm_force / 100000, BN = (g_gemm_force / 100) % 1000, sp = g_gemm_force % 100;
     const bool ok = (BM == 256 || BM == 128 || (BM == 64 && BN == 320 && sp == 1 && !a.gn_part)) &&
                     (BN == 320 || BN == 256 || BN == 128) && a.N % BN == 0 &&
-                    sp >= 1 && (sp == 1 || !((a.out_f32 && canon_batch(a) > 1) || a.geglu)) && (!a.geglu || BN % 128 == 0) &&
-                    !(BM == 256 && BN == 128);   // (256x128 is a 4x2-wave shape: not forced)
+                    sp >= 1 && (sp == 1 || !((a.out_f32 && canon_batch(a) > 1) || a.geglu)) && (!a.geglu || BN % 128 == 0);
     if (ok) {
       best.BM = BM; best.BN = BN; best.splits = sp; best.per = (nk + sp - 1) / sp;
       if ((long)(sp - 1) * best.per < nk) return best;

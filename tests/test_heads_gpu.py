@@ -123,3 +123,52 @@ def test_vae_heads_fused_vs_unfused(device, dtype):
         rel = float((res[0][k] - res[1][k]).norm() / res[1][k].norm())
         assert torch.isfinite(res[0][k]).all()
         assert rel < (1e-2 if dtype == "bf16" else 2e-3), (k, rel)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("res", [64, 40])
+def test_unet_up2_vs_resize_conv(device, dtype, res):
+    """The UNet's nearest-2x upsamplers as four per-parity 2x2 convs (option up2, default) vs the resize conv
+    (up2 0): the same real arithmetic (tests/test_ln_fold_host.py::test_conv_up2_parity_identity), the folded
+    weights rounded once to 16 bit.  res 40: latent sides not divisible by 8 (5x5 -> 10x10 -> 20x20 -> 40x40)."""
+    from tests import models_common as MC
+    from image_restoration_and_enhancement_amd.engine import UNet
+    pc, sd = MC.state_dicts("denoise")
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    unet = UNet(pc.unet, dtype, device)
+    unet.load_state_dict(sd["unet"])
+    g = torch.Generator().manual_seed(11)
+    xin = torch.zeros(2, res, res, unet.cin_pad)
+    xin[..., :4] = torch.randn(2, res, res, 4, generator=g)
+    xin = xin.to(tdt).to(device).contiguous()
+    kv = unet.prepare_context(torch.randn(2, 77, 768, generator=g).to(tdt).to(device).contiguous())
+    outs = []
+    for v in (1, 0):
+        with L.option(up2=v):
+            outs.append(unet.forward(xin, torch.full((2,), 481.0, device=device), kv, 77).float().cpu())
+    rel = float((outs[0] - outs[1]).norm() / outs[1].norm())
+    print(f"\nUNet up2 vs resize conv ({dtype}, {res}x{res}): rel L2 {rel:.2e}")
+    assert torch.isfinite(outs[0]).all()
+    assert rel < (2e-2 if dtype == "bf16" else 4e-3), rel
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_vae_decoder_up2_vs_resize_conv(device, dtype):
+    from tests import models_common as MC
+    from image_restoration_and_enhancement_amd.engine import VAE
+    pc, sd = MC.state_dicts("denoise")
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    vae = VAE(pc.vae, dtype, device)
+    vae.load_state_dict(sd["vae"])
+    g = torch.Generator().manual_seed(12)
+    z = torch.zeros(2, 16, 16, 8)
+    z[..., :4] = torch.randn(2, 16, 16, 4, generator=g)
+    z = z.to(tdt).to(device).contiguous()
+    outs = []
+    for v in (1, 0):
+        with L.option(up2=v):
+            outs.append(vae.decode(z).float().cpu())
+    rel = float((outs[0] - outs[1]).norm() / outs[1].norm())
+    print(f"\nVAE decoder up2 vs resize conv ({dtype}): rel L2 {rel:.2e}")
+    assert torch.isfinite(outs[0]).all()
+    assert rel < (3e-2 if dtype == "bf16" else 5e-3), rel
