@@ -79,6 +79,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gn_narrow", &g_gn_narrow, nullptr},
     {"attn_pf", &g_attn_pf, nullptr},
     {"attn_q2", &g_attn_q2, nullptr},
+    {"attn_pp", &g_attn_pp, nullptr},
     {"halo_split", &g_halo_split, nullptr},
     {"halo_pipe", &g_halo_pipe, nullptr},
     {"gemm_pp", &g_gemm_pp, nullptr},

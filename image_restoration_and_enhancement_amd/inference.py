@@ -17,9 +17,10 @@ Differences that follow from the engine (documented in INTEGRATION.md):
 * the diffusion path needs a ROCm GPU; on a CPU-only host the loaders fail and the classical fallbacks
   run (the reference would run diffusers on the CPU).  A missing or unloadable `libirx.so` is never
   hidden: `IrxError` propagates out of every entry point (no silent fallback).
-* compute dtype is bf16 on the GPU by default; `config["engine"] = {"dtype": "fp16"}` selects the
-  reference's own GPU dtype (src/inference.py:57) and `{"dtype": "fp32"}` the fp32 engine that matches the
-  reference CPU path within 1e-3 per pixel.
+* compute dtype is fp16 on the GPU by default, the reference's own GPU dtype (src/inference.py:57);
+  `config["engine"] = {"dtype": "bf16"}` selects the bf16 UNet / CLIP (the VAE stays fp16 unless
+  `{"vae_dtype": ...}` says otherwise: the bench configuration) and `{"dtype": "fp32"}` the fp32 engine that
+  matches the reference CPU path within 1e-3 per pixel.
 * noise is drawn from `torch.Generator("cpu").manual_seed(seed)` — the reference's CPU-path draws.
 * weights load from the task's saved `best/` directory (safetensors) or, in pretrained mode
   (`fine_tuned_dir == "nonexistent"`), from a local Hugging Face cache snapshot of `pretrained_id` (no

@@ -30,6 +30,17 @@ CONVS = [  # (label, N, H, W, C0, C1, Cout, k, stride, up)
     ("vae512@128", 8, 128, 128, 512, 0, 512, 3, 1, None),
     ("vae256@256", 8, 256, 256, 256, 0, 256, 3, 1, None),
     ("vae128@512", 8, 512, 512, 128, 0, 128, 3, 1, None),
+    # one parity of a nearest-2x upsampler as a 2x2 conv of the low-resolution input (IRX_LAYOUT_CONV_UP2)
+    ("up2p1280@8", 16, 8, 8, 1280, 0, 1280, 2, 1, None),
+    ("up2p1280@16", 16, 16, 16, 1280, 0, 1280, 2, 1, None),
+    ("up2p640@32", 16, 32, 32, 640, 0, 640, 2, 1, None),
+    ("vaeup2p512@64", 8, 64, 64, 512, 0, 512, 2, 1, None),
+    ("vaeup2p512@128", 8, 128, 128, 512, 0, 512, 2, 1, None),
+    ("vaeup2p256@256", 8, 256, 256, 256, 0, 256, 2, 1, None),
+    # ff.net.2 folded through proj_out: 1x1 conv over the concat (h | g)
+    ("chain320@64", 16, 64, 64, 320, 1280, 320, 1, 1, None),
+    ("chain640@32", 16, 32, 32, 640, 2560, 640, 1, 1, None),
+    ("chain1280@16", 16, 16, 16, 1280, 5120, 1280, 1, 1, None),
 ]
 GEMMS = [  # (label, M, N, K)
     ("lin320x320@64", 65536, 320, 320),
@@ -72,6 +83,9 @@ def main():
     ap.add_argument("--match", default="", help="only shapes whose label contains this")
     ap.add_argument("--ref", action="store_true", help="also time torch (hipBLASLt / MIOpen) on the same shapes")
     ap.add_argument("--variants", default="s2,ring64,small")
+    ap.add_argument("--attn-ko", type=lambda t: [int(x) for x in t.split(",")], default=[],
+                    help="attn3pp timing knock-outs to time beside the variants (results wrong): 8 exp2, 16 row "
+                         "max, 32 staging")
     args = ap.parse_args()
     dev = torch.device("cuda")
     L.load()
@@ -106,7 +120,8 @@ def main():
             res = []
             for vn, opts in variants:
                 setv(opts)
-                ms = timeit(lambda: O.conv2d(x0, w, b, x1=x1, up_hw=up), args.iters)
+                ms = timeit(lambda: O.conv2d(x0, w, b, pad=(k // 2, k // 2) if k != 2 else (1, 1), x1=x1, up_hw=up,
+                                             out_hw=(H, W) if k == 2 else None), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             if args.ref:   # MIOpen (torch) channels-last bf16 conv on the same data: a known-good reference
                 xr = (torch.cat([x0, x1], -1) if x1 is not None else x0).permute(0, 3, 1, 2)
@@ -140,8 +155,11 @@ def main():
             v = torch.randn(B, Lk, C, device=dev, generator=g).to(dt)
             flops = 4.0 * B * Lq * Lk * C
             res = []
-            for vn, opts in (("pf", {"attn_pf": 1, "attn_q2": 0}), ("nopf", {"attn_pf": 0, "attn_q2": 0}),
-                             ("q2", {"attn_pf": 1, "attn_q2": 1})):
+            for vn, opts in (("pf", {"attn_pf": 1, "attn_q2": 0, "attn_pp": 0}),
+                             ("q2", {"attn_pf": 1, "attn_q2": 1, "attn_pp": 0}),
+                             ("pp", {"attn_pp": 1}), ("pp_q2", {"attn_pp": 2}), ("pp_prio", {"attn_pp": 5}),
+                             ("pp_q2_prio", {"attn_pp": 6})) + tuple(
+                                 (f"ko{k}", {"attn_pp": 5 | k}) for k in args.attn_ko):
                 with L.option(**opts):
                     ms = timeit(lambda: O.attention(q, k, v, 8), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
