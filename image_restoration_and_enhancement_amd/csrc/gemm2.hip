@@ -1173,33 +1173,39 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       // LayerNorm partials of the output (GemmArgs::ln_out; host: gemm_emits_ln_parts, BN == kLnGroup): the final
       // values are written back over the staged tile, then G threads per row reduce it in two passes
       float2* const lno = BN == kLnGroup ? a.ln_out : nullptr;
-      // residual chunks requested kEpiPF iterations at a time (as in the GroupNorm-partial loop above)
-      // (the plain store pass keeps one chunk per step: prefetching here spilled the 256x320 tiles)
-      constexpr bool kPlainPF = false;
-      constexpr int KIT = kPlainPF ? (BM * CPR + NT - 1) / NT : 1;
-      constexpr int PF = kPlainPF ? kEpiPF : 1;
-      uint4 rres[PF];
-#pragma unroll 1
-      for (int k0 = 0; k0 < KIT; k0 += PF) {
-        if constexpr (kPlainPF) {
-          if (Rp) {
-#pragma unroll
-            for (int u = 0; u < PF; ++u) {
-              const int idx = min(tid + (k0 + u) * NT, BM * CPR - 1);
-              const int row = idx / CPR, c = idx - row * CPR;
-              const int m = min(m0 + row, a.M - 1), n = min(n0 + c * 8, a.N - 8);
-              rres[u] = *(const uint4*)(Rp + (long)m * a.ldr + n);
-            }
-          }
+      // head-split output (attention operands, GemmArgs::hs_L) with nothing to add: the tile's columns are whole
+      // heads of one q / k / v part and its rows one image's tokens, so each head segment of the tile is one
+      // contiguous [BM][hs_d] block of C.  Chunks are walked segment-major (consecutive lanes write consecutive
+      // 16-byte chunks of a segment: whole lines per wave store) with the segment base computed once, instead of
+      // c_off's three divides per chunk and stores scattered over every head of a row.
+      if (a.hs_L && !Rp && !a.rowadd && !lno && a.out_scale == 1.f && (a.hs_d & 7) == 0 && a.hs_L % BM == 0 &&
+          BN % a.hs_d == 0 && n0 % a.hs_d == 0 && a.hs_C % BN == 0 && m0 + BM <= a.M && n0 + BN <= a.N) {
+        const int dch = a.hs_d >> 3, segc = BM * dch;
+        const int part = n0 / a.hs_C, hd0 = (n0 - part * a.hs_C) / a.hs_d, heads = a.hs_C / a.hs_d;
+        const long img = m0 / a.hs_L, tok0 = m0 - img * a.hs_L;
+        uint16_t* const hb = Cp + (long)part * a.M * a.hs_C + ((img * heads + hd0) * a.hs_L + tok0) * a.hs_d;
+        const long sstride = (long)a.hs_L * a.hs_d;
+        const float inv_segc = 1.f / (float)segc, inv_dch = 1.f / (float)dch;
+#pragma unroll 2
+        for (int idx = tid; idx < BM * CPR; idx += NT) {
+          // idx = (seg, row, cc): float-reciprocal quotients corrected by one step (exact for idx < 2^24)
+          int seg = (int)((float)idx * inv_segc);
+          seg += (seg + 1) * segc <= idx;
+          seg -= seg * segc > idx;
+          const int rem = idx - seg * segc;
+          int row = (int)((float)rem * inv_dch);
+          row += (row + 1) * dch <= rem;
+          row -= row * dch > rem;
+          const int cc = rem - row * dch, c = seg * dch + cc;
+          *(uint4*)(hb + seg * sstride + (long)row * a.hs_d + cc * 8) =
+              *(const uint4*)(tileS + row * BN + (csw(c, row) << 3));
         }
-#pragma unroll
-      for (int pu = 0; pu < PF; ++pu) {
-      const int k = k0 + pu;
-#pragma unroll 1
-      for (int idx = tid + k * NT; idx < BM * CPR; idx += (kPlainPF ? BM * CPR : NT)) {
-        const int row = idx / CPR, c = idx - row * CPR;
+        return;
+      }
+      // one 16-byte chunk of the plain store pass: row add, residual, output scale; written back over the staged
+      // tile when the LayerNorm partials below read it
+      auto store_chunk = [&](int row, int c) {
         const int m = m0 + row, n = n0 + c * 8;
-        if (m >= a.M || n >= a.N) continue;
         uint4* const ts = (uint4*)(tileS + row * BN + (csw(c, row) << 3));
         uint4 u = *ts;
         if (Rp || a.rowadd || a.out_scale != 1.f) {
@@ -1212,7 +1218,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           }
           if (Rp) {
             float rv[8];
-            Vec16<T>::unpack(kPlainPF ? rres[pu] : *(const uint4*)(Rp + (long)m * a.ldr + n), rv);
+            Vec16<T>::unpack(*(const uint4*)(Rp + (long)m * a.ldr + n), rv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] += rv[e];
           }
@@ -1222,8 +1228,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           if (lno) *ts = u;
         }
         *(uint4*)(Cp + c_off(a, m, n)) = u;
-      }
-      }
+      };
+      // (one chunk per step: batching the residual loads of 8 steps measured no faster, 31.9 vs 31.9 us at the
+      //  64^2-level to_out shape, profiles/r05_kbench_gemm_res.txt)
+#pragma unroll 1
+      for (int idx = tid; idx < BM * CPR; idx += NT) {
+        const int row = idx / CPR, c = idx - row * CPR;
+        if (m0 + row >= a.M || n0 + c * 8 >= a.N) continue;
+        store_chunk(row, c);
       }
       if constexpr (BN == kLnGroup && NT % BM == 0) {
         if (lno) {
@@ -1411,17 +1423,20 @@ void launch2_t(const GemmArgs& a, const Split& sp, hipStream_t s) {
   if (prof_on() && g_prof_shapes)
     nm += " [M " + std::to_string(a.M) + " N " + std::to_string(a.N) + " K " + std::to_string(a.K) +
           (a.conv ? " conv " + std::to_string(a.g.Hin) + "x" + std::to_string(a.g.Win) : std::string()) +
-          " split " + std::to_string(sp.splits) + (a.geglu ? " geglu" : "") + "]";
+          " split " + std::to_string(sp.splits) + (a.geglu ? " geglu" : "") + (a.residual ? " res" : "") +
+          (a.ln_rs || a.ln_part ? " lnfold" : "") + (a.ln_out ? " lnout" : "") + (a.b_rows ? " bimg" : "") +
+          (a.gn_part ? " gnpart" : "") + (a.up2_w ? " up2" : "") + "]";
+  const GemmArgs& ea = a;
   {
     ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
     if constexpr (HALO != 0) {
-      gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false, HALO><<<grid, block, 0, s>>>(a, sp);
+      gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false, HALO><<<grid, block, 0, s>>>(ea, sp);
     } else if (a.conv) {   // (fp32-output convs never take this path: see eligible())
-      if (rs) gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, true, 0, PP><<<grid, block, 0, s>>>(a, sp);
-      else gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false, 0, PP><<<grid, block, 0, s>>>(a, sp);
+      if (rs) gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, true, 0, PP><<<grid, block, 0, s>>>(ea, sp);
+      else gemm2_kernel<T, BM, BN, WM, WN, BK, S, true, false, false, 0, PP><<<grid, block, 0, s>>>(ea, sp);
     } else {
-      if (a.out_f32) gemm2_kernel<T, BM, BN, WM, WN, BK, S, false, true, false, 0, PP><<<grid, block, 0, s>>>(a, sp);
-      else gemm2_kernel<T, BM, BN, WM, WN, BK, S, false, false, false, 0, PP><<<grid, block, 0, s>>>(a, sp);
+      if (a.out_f32) gemm2_kernel<T, BM, BN, WM, WN, BK, S, false, true, false, 0, PP><<<grid, block, 0, s>>>(ea, sp);
+      else gemm2_kernel<T, BM, BN, WM, WN, BK, S, false, false, false, 0, PP><<<grid, block, 0, s>>>(ea, sp);
     }
     IRX_LAUNCH_CHECK();
   }

@@ -226,26 +226,34 @@ __global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const double2* _
   const int n = blockIdx.x, t = threadIdx.x;
   const int C = C0 + C1, cg = C / G;
   const int gl = t >> 5, sub = t & 31, g = blockIdx.y * 8 + gl;
+  // this thread's output channel's gamma / beta, loaded up front (their latency hides under the fold)
+  const int c0 = blockIdx.y * 8 * cg, c1 = min(C, c0 + 8 * cg);
+  const bool own = c0 + t < c1 && 8 * cg <= 256;
+  const float gam = own ? gamma[c0 + t] : 0.f, bet = own ? beta[c0 + t] : 0.f;
   double a = 0.0, b = 0.0;
   if (g < G) {
     // the group's channels [g*cg, g*cg + cg) split at the concat seam: c0s channels from x0, the rest from x1
     const int cb = g * cg, c0s = max(0, min(cg, C0 - cb));
     const int tot0 = rpi0 * c0s, tot1 = rpi1 * (cg - c0s);
+    // item i = (row block i / cs, channel i % cs) walked with an incremental (row, channel) pair: no divide per item
+    auto fold = [&](const double2* __restrict__ p, int rpi, int Cs, int cbase, int cs, int tot) {
+      if (tot <= 0) return;
+      int r = sub / cs, ch = sub - r * cs;
+      const int dr = 32 / cs, dch = 32 - dr * cs;
+      const double2* base = p + (long)n * rpi * Cs + cbase;
 #pragma unroll 4
-    for (int i = sub; i < tot0; i += 32) {
-      const int r = i / c0s, ch = cb + (i - r * c0s);
-      const double2 v = p0[((long)n * rpi0 + r) * C0 + ch];
-      a += v.x;
-      b += v.y;
-    }
+      for (int i = sub; i < tot; i += 32) {
+        const double2 v = base[(long)r * Cs + ch];
+        a += v.x;
+        b += v.y;
+        r += dr;
+        ch += dch;
+        if (ch >= cs) { ch -= cs; ++r; }
+      }
+    };
+    fold(p0, rpi0, C0, cb, c0s, tot0);
     const int c1b = cb + c0s - C0, c1s = cg - c0s;
-#pragma unroll 4
-    for (int i = sub; i < tot1; i += 32) {
-      const int r = i / c1s, ch = c1b + (i - r * c1s);
-      const double2 v = p1[((long)n * rpi1 + r) * C1 + ch];
-      a += v.x;
-      b += v.y;
-    }
+    fold(p1, rpi1, C1, c1b, c1s, tot1);
   }
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
@@ -257,11 +265,18 @@ __global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const double2* _
     if (mr) mr[(long)n * G + g] = gmr[gl];
   }
   __syncthreads();
-  const int c0 = blockIdx.y * 8 * cg, c1 = min(C, c0 + 8 * cg);
-  for (int c = c0 + t; c < c1; c += 256) {
-    const float2 r = gmr[(c - c0) / cg];
-    const float sc = r.y * gamma[c];
-    ab[(long)n * C + c] = make_float2(sc, fmaf(-r.x, sc, beta[c]));
+  if (8 * cg <= 256) {
+    if (own) {
+      const float2 r = gmr[t / cg];
+      const float sc = r.y * gam;
+      ab[(long)n * C + c0 + t] = make_float2(sc, fmaf(-r.x, sc, bet));
+    }
+  } else {
+    for (int c = c0 + t; c < c1; c += 256) {
+      const float2 r = gmr[(c - c0) / cg];
+      const float sc = r.y * gamma[c];
+      ab[(long)n * C + c] = make_float2(sc, fmaf(-r.x, sc, beta[c]));
+    }
   }
 }
 

@@ -54,6 +54,10 @@ GEMMS = [  # (label, M, N, K)
     ("ff2@32", 16384, 640, 2560),
     ("lin1280@16", 4096, 1280, 1280),
     ("ff1@16", 4096, 10240, 1280),
+    # + residual (attn to_out at each level: the store pass reads the residual stream)
+    ("lin320x320@64+res", 65536, 320, 320, "res"),
+    ("lin640x640@32+res", 16384, 640, 640, "res"),
+    ("lin1280@16b+res", 4096, 1280, 1280, "res"),
 ]
 ATTNS = [  # (label, B, L, Lk, C)
     ("self d40 L4096", 16, 4096, 4096, 320),
@@ -133,14 +137,18 @@ def main():
                 res.append(f"miopen {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             print(f"{lab:24s} " + " | ".join(res), flush=True)
     if args.only in ("", "gemm"):
-        for lab, M, N, K in GEMMS:
+        for lab, M, N, K, *extra in GEMMS:
+            if args.match not in lab:
+                continue
             A = torch.randn(M, K, device=dev, generator=g).to(dt)
             Bw = (torch.randn(N, K, device=dev, generator=g) / math.sqrt(K)).to(dt)
+            R = torch.randn(M, N, device=dev, generator=g).to(dt) if "res" in extra else None
+            bias = torch.zeros(N, device=dev) if R is not None else None
             flops = 2.0 * M * N * K
             res = []
             for vn, opts in variants:
                 setv(opts)
-                ms = timeit(lambda: O.gemm(A, Bw), args.iters)
+                ms = timeit(lambda: O.gemm(A, Bw, bias=bias, residual=R), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             if args.ref:   # hipBLASLt (torch.matmul) on the same data: a known-good reference
                 Bt = Bw.t()

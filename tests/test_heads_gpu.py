@@ -172,3 +172,29 @@ def test_vae_decoder_up2_vs_resize_conv(device, dtype):
     print(f"\nVAE decoder up2 vs resize conv ({dtype}): rel L2 {rel:.2e}")
     assert torch.isfinite(outs[0]).all()
     assert rel < (3e-2 if dtype == "bf16" else 5e-3), rel
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("res", [64, 40])
+def test_unet_head_major_operands_bit_exact(device, dtype, res):
+    """q|k|v written head-major by the projection epilogue (option attn_hm, default; the segment-major coalesced
+    store walk of gemm2's store pass) vs row-major operands: the same values in another layout, read by the same
+    attention arithmetic — the UNet output is identical bit for bit.  res 40: 5x5 .. 40x40 levels (tiles that the
+    segment walk refuses: rows of one tile spanning two images fall back to the per-chunk c_off stores)."""
+    from tests import models_common as MC
+    from image_restoration_and_enhancement_amd.engine import UNet
+    pc, sd = MC.state_dicts("denoise")
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    unet = UNet(pc.unet, dtype, device)
+    unet.load_state_dict(sd["unet"])
+    g = torch.Generator().manual_seed(13)
+    xin = torch.zeros(2, res, res, unet.cin_pad)
+    xin[..., :4] = torch.randn(2, res, res, 4, generator=g)
+    xin = xin.to(tdt).to(device).contiguous()
+    kv = unet.prepare_context(torch.randn(2, 77, 768, generator=g).to(tdt).to(device).contiguous())
+    outs = []
+    for v in (1, 0):
+        with L.option(attn_hm=v):
+            outs.append(unet.forward(xin, torch.full((2,), 481.0, device=device), kv, 77).float().cpu())
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
