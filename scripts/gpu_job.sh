@@ -9,6 +9,8 @@
 #   smoke                               __graft_entry__.smoke()
 #   bench|<name>|<bench.py args>        bench line -> <name>.json, log -> <name>.err
 #   prof|<name>|<bench.py args>         rocprofv3 --kernel-trace --stats of bench.py -> <name>_kernel_stats.csv
+#   trace|<name>|<bench.py args>        rocprofv3 --kernel-trace of bench.py, GPU idle inside the last two steps
+#                                       (scripts/step_gaps.py) -> <name>.txt
 #   pmc|<name>|<pmc_top.py run args>    PMC passes of the bench's top kernels (scripts/pmc_top.py) -> <name>.json
 #   kpmc|<name>|<regex>|<counters>|<kprof.py args>   one rocprofv3 --pmc pass over scripts/kprof.py (one hot op looped),
 #                                       kernels matching <regex> -> <name>.txt (mean per dispatch, scripts/pmc_dump.py)
@@ -52,6 +54,13 @@ for step in "$@"; do
       f=$(find "$O/prof_$name" -name "*kernel_stats.csv" | head -1)
       cp "$f" "$O/${name}_kernel_stats.csv" && rm -rf "$O/prof_$name"
       head -12 "$O/${name}_kernel_stats.csv" | cut -c1-200 ;;
+    trace)
+      timeout -k 10 "$lim" rocprofv3 --kernel-trace --output-format csv -d "$O/trace_$name" -o tr -- \
+        python3 bench.py $rest > "$O/$name.log" 2>&1
+      rc=$?; [ $rc -eq 0 ] || { tail "$O/$name.log"; fail "$name" $rc; }
+      f=$(find "$O/trace_$name" -name "*kernel_trace.csv" | head -1)
+      python3 scripts/step_gaps.py "$f" --steps 2 > "$O/$name.txt"; cat "$O/$name.txt"
+      rm -rf "$O/trace_$name" ;;
     pmc)
       timeout -k 10 "$lim" python3 scripts/pmc_top.py run --dir "$O/pmc_$name" $rest
       rc=$?; [ $rc -eq 0 ] || fail "$name" $rc
