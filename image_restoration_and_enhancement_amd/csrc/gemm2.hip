@@ -947,7 +947,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       constexpr int CPR = BN / 8;               // 16-byte chunks per row
       // residual / row-add operands of the store passes requested before the first store (not for the 128x128 tiles:
       // two of them stay resident per CU only within 128 VGPRs)
-      // (halo conv tiles only: the GroupNorm-partial loop of the 256x320 tiles spilled with it)
+      // (halo conv tiles only: the GroupNorm-partial loop of the 256x320 tiles spilled with it; on the 128x320
+      //  tiles of proj_out ∘ ff.net.2 at 32^2 / 16^2 it measured no faster, profiles/r05_bench_shapes_chain.txt)
       constexpr bool kEpiPrefetch = HALO != 0;
       constexpr int kEpiPF = 4;
       // chunk swizzle inside whole groups of 8 chunks only (BN = 160 leaves a 4-chunk tail unswizzled)

@@ -55,6 +55,8 @@ GEMMS = [  # (label, M, N, K)
     ("lin1280@16", 4096, 1280, 1280),
     ("ff1@16", 4096, 10240, 1280),
     # + residual (attn to_out at each level: the store pass reads the residual stream)
+    ("chain-as-gemm@32", 16384, 640, 3200),
+    ("chain-as-gemm@16", 4096, 1280, 6400),
     ("lin320x320@64+res", 65536, 320, 320, "res"),
     ("lin640x640@32+res", 16384, 640, 640, "res"),
     ("lin1280@16b+res", 4096, 1280, 1280, "res"),
