@@ -80,6 +80,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"attn_pf", &g_attn_pf, nullptr},
     {"attn_q2", &g_attn_q2, nullptr},
     {"attn_pp", &g_attn_pp, nullptr},
+    {"conv1x1_dense", &g_conv1x1_dense, nullptr},
     {"halo_split", &g_halo_split, nullptr},
     {"halo_pipe", &g_halo_pipe, nullptr},
     {"gemm_pp", &g_gemm_pp, nullptr},
@@ -552,6 +553,7 @@ int irx_op_conv2d(void* s, int dtype, const void* x0, const void* x1, int c0, in
   a.residual = residual; a.ldr = cout;
   a.act = act;
   a.imgs = n;   // image-indexed: the same tile / split choice as the models make for this per-image shape
+  conv1x1_as_dense(a);   // as the models do
   gemm(a, S(s));
   IRX_API_END
 }

@@ -279,6 +279,8 @@ void gemm(const GemmArgs& a, hipStream_t s) {
     IRX_CHECK(g.Hv >= g.Hin && g.Wv >= g.Win, "virtual (upsampled) size must not shrink");
   } else {
     IRX_CHECK(a.A && a.lda % vec == 0 && ((uintptr_t)a.A % 16) == 0, "A rows must be 16-byte aligned");
+    IRX_CHECK(!a.A1 || (a.batch == 1 && a.kA1 > 0 && a.kA1 < a.K && a.lda1 % vec == 0 && ((uintptr_t)a.A1 % 16) == 0),
+              "second A source: batch 1, 0 < kA1 < K, 16-byte rows");
   }
   IRX_CHECK(!(a.ln_rs || a.ln_part) || (a.ln_u && gemm_ln_foldable(a)), "folded LayerNorm needs the large-tile path");
   IRX_CHECK(!a.ln_part || (a.ln_T >= 1 && a.K == a.ln_T * kLnGroup), "LayerNorm partials must cover the K row");
@@ -304,6 +306,7 @@ void gemm(const GemmArgs& a, hipStream_t s) {
     return;
   }
   if (a.dtype != F32 && g_large_tiles && gemm_large_tile(a, s)) return;
+  IRX_CHECK(!a.A1, "a two-source A (conv1x1_as_dense) needs the large-tile path");
   if (a.dtype == F32) launch_t<float>(a, s);
   else if (a.dtype == F16) launch_t<f16_t>(a, s);
   else launch_t<bf16_t>(a, s);

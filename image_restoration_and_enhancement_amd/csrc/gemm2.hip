@@ -146,6 +146,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   const uint16_t* __restrict__ Bp = (const uint16_t*)a.B + (long)z * a.sB + bimg * a.b_img_stride;
   const float* __restrict__ biasp = a.bias ? a.bias + bimg * a.bias_img_stride : nullptr;
   const uint16_t* __restrict__ Ap = CONV ? nullptr : (const uint16_t*)a.A + (long)z * a.sA;
+  const uint16_t* const A1p = CONV ? nullptr : (const uint16_t*)a.A1;   // second A source from K = kA1 (batch 1)
   const uint16_t* zp = (const uint16_t*)g_zero_page;
 
   // ---- per-lane DMA assignment: instruction q = wave*IPW + j covers rows RPI*q .. +RPI-1;
@@ -158,6 +159,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   int lk[IPW];                       // this lane's element offset in the K step (logical chunk * 8)
   int rn[IPW], riy[IPW], rix[IPW];   // conv A rows: image index (-1 invalid), receptive-field origin
   const uint16_t* rb[IPW];           // current row base (nullptr if out of range / padded tap)
+  int arow[IPW];                     // dense A rows: the row index m (-1 invalid), for the switch to A1
 #pragma unroll
   for (int j = 0; j < IPW; ++j) {
     const int q = wave * IPW + j;
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     live[j] = q < NINST;
     isA[j] = live[j] && r < BM;
     lk[j] = (lslot ^ swz(r)) * 8;
-    rn[j] = -1; riy[j] = 0; rix[j] = 0; rb[j] = nullptr;
+    rn[j] = -1; riy[j] = 0; rix[j] = 0; rb[j] = nullptr; arow[j] = -1;
     if (!live[j]) continue;
     if (r < BM) {
       const int m = m0 + r;
@@ -178,7 +180,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           riy[j] = oy * a.g.stride - a.g.pad_t;
           rix[j] = ox * a.g.stride - a.g.pad_l;
         } else {
-          rb[j] = Ap + (long)m * a.lda;
+          arow[j] = m;
+          rb[j] = (A1p && kt0 * BK >= a.kA1) ? A1p + (long)m * a.lda1 : Ap + (long)m * a.lda;
         }
       }
     } else {
@@ -219,7 +222,17 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 
   auto issue = [&](int kt, int stage) {
     uint4* sbase = smem + stage * STAGE;
-    const int koffA = CONV ? (kc >= a.g.C0 ? kc - a.g.C0 : kc) : kt * BK;
+    int koffA = CONV ? (kc >= a.g.C0 ? kc - a.g.C0 : kc) : kt * BK;
+    if constexpr (!CONV) {
+      if (A1p && koffA >= a.kA1) {      // the concat's second source (steps are issued in order: one switch)
+        if (koffA == a.kA1 && kt != kt0) {
+#pragma unroll
+          for (int j = 0; j < IPW; ++j)
+            if (isA[j] && arow[j] >= 0) rb[j] = A1p + (long)arow[j] * a.lda1;
+        }
+        koffA -= a.kA1;
+      }
+    }
     const int koffB = kt * BK;
 #pragma unroll
     for (int j = 0; j < IPW; ++j) {
@@ -1592,6 +1605,7 @@ bool eligible(const GemmArgs& a) {
   if (canon_rows(a) < 512) return false;           // tiny outputs: the 64x64 4-wave tiles waste less
   if (a.geglu && (a.out_f32 || a.residual || a.batch != 1 || a.N % 128 != 0)) return false;
   if (a.conv) return !a.out_f32 && a.g.C0 % bk == 0 && a.g.C1 % bk == 0;
+  if (a.A1 && (a.batch != 1 || a.kA1 % 64 != 0 || a.lda1 % 8 != 0 || ((uintptr_t)a.A1 % 16) != 0)) return false;
   return a.lda % 8 == 0 && (a.batch == 1 || a.sA % 8 == 0);
 }
 
@@ -1617,6 +1631,23 @@ int halo_bn(const GemmArgs& a);
 
 bool gemm_gn_fusable(const GemmArgs& a) {
   return g_gn_fuse && g_large_tiles && is16(a.dtype) && eligible(a) && halo_bn(a) != 0;
+}
+
+int g_conv1x1_dense = 1;   // irx_set_option("conv1x1_dense", 0): 1x1 convs on the im2col conv path (A/B)
+
+bool conv1x1_as_dense(GemmArgs& a) {
+  const ConvGeom& g = a.g;
+  if (!g_conv1x1_dense || !a.conv || !is16(a.dtype) || a.batch != 1 || a.gn_ab || a.up2_w || a.act != ACT_NONE) return false;
+  if (g.KH != 1 || g.KW != 1 || g.stride != 1 || g.pad_t != 0 || g.pad_l != 0) return false;
+  if (g.Hv != g.Hin || g.Wv != g.Win || g.Ho != g.Hin || g.Wo != g.Win) return false;
+  GemmArgs d = a;
+  d.conv = 0;
+  d.g = ConvGeom();
+  d.A = g.src0; d.lda = g.C0;
+  d.A1 = g.C1 ? g.src1 : nullptr; d.lda1 = g.C1; d.kA1 = g.C1 ? g.C0 : 0;
+  if (!g_large_tiles || !eligible(d) || choose(d).BM == 0) return false;
+  a = d;
+  return true;
 }
 
 int g_gn_parts = 1;
@@ -1833,6 +1864,7 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     if (c.BN == 160) launch2<128, 160, 2, 2, 64, 2>(b, sp, s);
     else launch2<128, 128, 2, 2, 64, 2>(b, sp, s);
   } else if (g_gemm_deep == 0 &&
+             !a.A1 &&   // (the lean dense ping-pong addresses one A source)
              (g_gemm_pp == 1 || (g_gemm_pp >= 2 && !a.conv && c.BM == 256 && (c.BN == 256 || (g_gemm_pp == 3 && c.BN == 320)) &&
                                  !a.ln_out && !a.b_rows)) &&
              (a.conv || (a.M % c.BM == 0 && a.N % c.BN == 0))) {

@@ -133,6 +133,7 @@ static GemmArgs conv_args(int dt, const Act& x0, const Act* x1, const void* w, c
   a.rowadd = rowadd; a.rowadd_ld = rowadd_ld; a.rows_per_group = out.h * out.w;
   a.residual = residual; a.ldr = a.ldc;
   a.imgs = out.n;
+  conv1x1_as_dense(a);   // 1x1 convs (ff chains, resnet shortcuts) on the dense GEMM path
   return a;
 }
 

@@ -25,6 +25,9 @@ struct GemmArgs {
   int conv = 0;           // 1: A is an implicit im2col of `g`
   ConvGeom g;
   const void* A = nullptr; long lda = 0; long sA = 0;    // dense A (+ batch stride)
+  // dense A's second source (a 1x1 conv over a channel concat, conv1x1_as_dense): A[m][k] = A1[m][k - kA1] for
+  // k >= kA1 (kA1 a multiple of the K step; batch 1; the generic large-tile loops only)
+  const void* A1 = nullptr; long lda1 = 0; int kA1 = 0;
   const void* B = nullptr; long ldb = 0; long sB = 0;
   void* C = nullptr; long ldc = 0; long sC = 0;
   int out_f32 = 0;        // C stored as fp32 regardless of dtype
@@ -137,6 +140,11 @@ __host__ __device__ __forceinline__ long c_off_f(long m, int n, long ldc, int M,
 bool gemm_up2_ok(const GemmArgs& a);   // the large-tile path can store a sub-pixel (GemmArgs::up2_*) output
 void gemm(const GemmArgs& a, hipStream_t s);
 bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path; false if not eligible
+// A 1x1 / stride-1 / unpadded conv (optionally over a channel concat) rewritten as a dense GEMM over the NHWC
+// rows (A = src0, A1 = src1 from K = C0) when the large-tile path takes it (option conv1x1_dense): the
+// im2col walk's per-tap machinery buys nothing at one tap.  Returns whether `a` was rewritten.
+bool conv1x1_as_dense(GemmArgs& a);
+extern int g_conv1x1_dense;
 bool gemm_sk(const GemmArgs& a, hipStream_t s);           // K = 320 streaming path (gemm_sk.hip); false if not eligible
 bool gemm_sk_eligible(const GemmArgs& a);
 extern int g_gemm_sk;      // 1: the K = 320 projections take gemm_sk (0: the large-tile kernel, A/B)

@@ -742,3 +742,39 @@ def test_attention_ping_pong_d40_bit_exact(device, dt, pp, B, Lq, Lk):
         base = O.attention(qd, kd, vd, heads)
     torch.cuda.synchronize()
     assert torch.equal(got, base)
+
+
+@pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("N,H,W,C0,C1,Co,res", [
+    (2, 64, 64, 320, 1280, 320, True),     # proj_out ∘ ff.net.2 at 64^2 (the ff chain, + residual)
+    (2, 32, 32, 640, 2560, 640, True),     # ... at 32^2
+    (4, 16, 16, 1280, 5120, 1280, True),   # ... at 16^2 (split-K)
+    (2, 32, 32, 1280, 640, 640, False),    # up-block resnet shortcut over the skip concat
+    (2, 64, 64, 640, 0, 320, False),       # single-source 1x1
+    (3, 7, 9, 320, 1280, 320, True),       # ragged rows (M = 189: a partial tile)
+])
+def test_conv1x1_two_source_dense(device, dt, N, H, W, C0, C1, Co, res):
+    """1x1 convs over a channel concat as a dense GEMM with a second A source from K = C0 (option conv1x1_dense,
+    default; conv1x1_as_dense) vs PyTorch fp32 on the same rounded operands, and vs the im2col conv path (option
+    off): the same per-output K order, so equal up to a different split choice."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    x0 = _r(N, C0, H, W, seed=90)
+    x1 = _r(N, C1, H, W, seed=91) if C1 else None
+    w = _r(Co, C0 + C1, 1, 1, seed=92, scale=1 / math.sqrt(C0 + C1))
+    b = _r(Co, seed=93)
+    r = _r(N, H, W, Co, seed=94) if res else None
+    d0 = _dev(x0.permute(0, 2, 3, 1), dt, device)
+    d1 = _dev(x1.permute(0, 2, 3, 1), dt, device) if C1 else None
+    dr = _dev(r, dt, device) if res else None
+    outs = []
+    for v in (1, 0):
+        with L.option(conv1x1_dense=v):
+            outs.append(O.conv2d(d0, w.to(dt).float(), b, pad=(0, 0), x1=d1, residual=dr))
+    torch.cuda.synchronize()
+    xin = torch.cat([_q(x0, dt)] + ([_q(x1, dt)] if C1 else []), 1)
+    ref = F.conv2d(xin, _q(w, dt), b).permute(0, 2, 3, 1)
+    if res:
+        ref = ref + _q(r, dt)
+    assert torch.isfinite(outs[0].float()).all()
+    assert O.rel_err(outs[0], ref) < TOL[dt]
+    assert O.rel_err(outs[0], outs[1].float()) < 2e-3
