@@ -213,25 +213,15 @@ __global__ __launch_bounds__(256) void gn_finalize3_kernel(const double* __restr
   }
 }
 
-// GroupNorm from producer partials (GemmArgs::gn_part): per (image, group of 8 GroupNorm groups) block, 32
-// threads per group fold the image's row-block partials of the group's channels (x0 then x1, fixed order)
-// in fp64 -> (mean, rstd) -> the channels' scale / shift.  Replaces the statistics pass over the tensor.
-__global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const double2* __restrict__ p0, int C0, int rpi0,
-                                                                const double2* __restrict__ p1, int C1, int rpi1,
-                                                                int G, double cnt, float eps,
-                                                                const float* __restrict__ gamma,
-                                                                const float* __restrict__ beta,
-                                                                float2* __restrict__ ab, float2* __restrict__ mr) {
-  __shared__ float2 gmr[8];
-  const int n = blockIdx.x, t = threadIdx.x;
-  const int C = C0 + C1, cg = C / G;
-  const int gl = t >> 5, sub = t & 31, g = blockIdx.y * 8 + gl;
-  // this thread's output channel's gamma / beta, loaded up front (their latency hides under the fold)
-  const int c0 = blockIdx.y * 8 * cg, c1 = min(C, c0 + 8 * cg);
-  const bool own = c0 + t < c1 && 8 * cg <= 256;
-  const float gam = own ? gamma[c0 + t] : 0.f, bet = own ? beta[c0 + t] : 0.f;
+// One (image n, group g)'s statistics from producer partials (GemmArgs::gn_part): 32 lanes (sub = lane in the group)
+// fold the image's row-block partials of the group's channels (x0 then x1, fixed order) in fp64, an xor-shuffle
+// sums the lanes, and every lane returns (mean, rstd).  The one definition gn_finalize_parts_kernel and gn_fa_kernel
+// share (bit-identical statistics on either path).  Called by every lane of the wave (the shuffles).
+__device__ __forceinline__ float2 gn_parts_fold(const double2* __restrict__ p0, int C0, int rpi0,
+                                                const double2* __restrict__ p1, int C1, int rpi1, int n, int g,
+                                                bool valid, int cg, int sub, double cnt, float eps) {
   double a = 0.0, b = 0.0;
-  if (g < G) {
+  if (valid) {
     // the group's channels [g*cg, g*cg + cg) split at the concat seam: c0s channels from x0, the rest from x1
     const int cb = g * cg, c0s = max(0, min(cg, C0 - cb));
     const int tot0 = rpi0 * c0s, tot1 = rpi1 * (cg - c0s);
@@ -257,26 +247,109 @@ __global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const double2* _
   }
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
+  const double mean = a / cnt;
+  double var = b / cnt - mean * mean;
+  if (var < 0.0) var = 0.0;
+  return make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+}
+
+// GroupNorm from producer partials: per (image, group of 8 GroupNorm groups) block, 32 threads per group
+// (gn_parts_fold) -> (mean, rstd) -> the channels' scale / shift.  Replaces the statistics pass over the tensor.
+__global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const double2* __restrict__ p0, int C0, int rpi0,
+                                                                const double2* __restrict__ p1, int C1, int rpi1,
+                                                                int G, double cnt, float eps,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta,
+                                                                float2* __restrict__ ab, float2* __restrict__ mr) {
+  __shared__ float2 gmr[8];
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int C = C0 + C1, cg = C / G;
+  const int gl = t >> 5, sub = t & 31, g = blockIdx.y * 8 + gl;
+  // this thread's output channel's gamma / beta, loaded up front (their latency hides under the fold)
+  const int c0 = blockIdx.y * 8 * cg, c1 = min(C, c0 + 8 * cg);
+  const bool own = c0 + t < c1 && 8 * cg <= 256;
+  const float gam = own ? gamma[c0 + t] : 0.f, bet = own ? beta[c0 + t] : 0.f;
+  const float2 r = gn_parts_fold(p0, C0, rpi0, p1, C1, rpi1, n, g, g < G, cg, sub, cnt, eps);
   if (sub == 0 && g < G) {
-    const double mean = a / cnt;
-    double var = b / cnt - mean * mean;
-    if (var < 0.0) var = 0.0;
-    gmr[gl] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
-    if (mr) mr[(long)n * G + g] = gmr[gl];
+    gmr[gl] = r;
+    if (mr) mr[(long)n * G + g] = r;
   }
   __syncthreads();
   if (8 * cg <= 256) {
     if (own) {
-      const float2 r = gmr[t / cg];
-      const float sc = r.y * gam;
-      ab[(long)n * C + c0 + t] = make_float2(sc, fmaf(-r.x, sc, bet));
+      const float2 q = gmr[t / cg];
+      const float sc = q.y * gam;
+      ab[(long)n * C + c0 + t] = make_float2(sc, fmaf(-q.x, sc, bet));
     }
   } else {
     for (int c = c0 + t; c < c1; c += 256) {
-      const float2 r = gmr[(c - c0) / cg];
-      const float sc = r.y * gamma[c];
-      ab[(long)n * C + c] = make_float2(sc, fmaf(-r.x, sc, beta[c]));
+      const float2 q = gmr[(c - c0) / cg];
+      const float sc = q.y * gamma[c];
+      ab[(long)n * C + c] = make_float2(sc, fmaf(-q.x, sc, beta[c]));
     }
+  }
+}
+
+// GroupNorm from producer partials, statistics and application in ONE launch for the small levels (HW <= 256: the
+// UNet's 16^2 / 8^2 tensors, option gn_fa): block = (image n, GPB consecutive groups); its lanes fold the groups'
+// partials exactly as gn_finalize_parts_kernel does (gn_parts_fold), the channels' scale / shift go to LDS, then
+// the block applies them (gn_act, as gn_apply_kernel) to its channels of every pixel, 16-byte chunks, four loads in
+// flight per thread.  Bit-identical to gn_finalize_parts_kernel + gn_apply_kernel; one launch and one tiny kernel's
+// ramp / drain fewer per GroupNorm.
+template <typename T>
+__global__ __launch_bounds__(256) void gn_fa_kernel(const double2* __restrict__ p0, int C0, int rpi0,
+                                                    const double2* __restrict__ p1, int C1, int rpi1, int G, int gpb,
+                                                    double cnt, float eps, const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, const T* __restrict__ x0,
+                                                    const T* __restrict__ x1, int HW, int silu, T* __restrict__ out) {
+  constexpr int VEC = 16 / (int)sizeof(T);
+  __shared__ float2 gmr[8];
+  __shared__ float2 sab[256];
+  const int n = blockIdx.y, t = threadIdx.x;
+  const int C = C0 + C1, cg = C / G;
+  const int gl = t >> 5, sub = t & 31, g = blockIdx.x * gpb + gl;
+  const int c0 = blockIdx.x * gpb * cg, nc = gpb * cg;
+  const float gam = t < nc ? gamma[c0 + t] : 0.f, bet = t < nc ? beta[c0 + t] : 0.f;
+  const float2 r = gn_parts_fold(p0, C0, rpi0, p1, C1, rpi1, n, g, gl < gpb, cg, sub, cnt, eps);
+  if (sub == 0 && gl < gpb) gmr[gl] = r;
+  __syncthreads();
+  if (t < nc) {
+    const float2 q = gmr[t / cg];
+    const float sc = q.y * gam;
+    sab[t] = make_float2(sc, fmaf(-q.x, sc, bet));
+  }
+  __syncthreads();
+  const int nch = nc / VEC, tot = HW * nch;
+  auto src_of = [&](int idx, int& k) -> const T* {
+    const int p = idx / nch;
+    k = idx - p * nch;
+    const int c = c0 + k * VEC;
+    return c < C0 ? x0 + ((long)n * HW + p) * C0 + c : x1 + ((long)n * HW + p) * C1 + (c - C0);
+  };
+  auto one = [&](const uint4& u, int idx, int k) {
+    float f[VEC];
+    Vec16<T>::unpack(u, f);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const float2 q = sab[k * VEC + e];
+      f[e] = gn_act(f[e], q.x, q.y, silu);
+    }
+    const int p = idx / nch;
+    *(uint4*)(out + ((long)n * HW + p) * C + c0 + k * VEC) = Vec16<T>::pack(f);
+  };
+  int idx = t;
+  for (; idx + 3 * 256 < tot; idx += 4 * 256) {   // four 16-byte loads in flight per thread
+    int k0, k1, k2, k3;
+    const uint4 u0 = *(const uint4*)src_of(idx, k0);
+    const uint4 u1 = *(const uint4*)src_of(idx + 256, k1);
+    const uint4 u2 = *(const uint4*)src_of(idx + 512, k2);
+    const uint4 u3 = *(const uint4*)src_of(idx + 768, k3);
+    one(u0, idx, k0); one(u1, idx + 256, k1); one(u2, idx + 512, k2); one(u3, idx + 768, k3);
+  }
+  for (; idx < tot; idx += 256) {
+    int k;
+    const uint4 u = *(const uint4*)src_of(idx, k);
+    one(u, idx, k);
   }
 }
 
@@ -461,6 +534,21 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
           const float* beta, int silu, void* out, void* ws, hipStream_t s, const double* p0 = nullptr, int r0 = 0,
           const double* p1 = nullptr, int r1 = 0) {
   float2* ab = gn_ab_ws(ws, N, G);
+  if (p0 && g_gn_fa && HW <= 256) {
+    // small levels: statistics + application in one launch (gn_fa_kernel); GPB groups per block so that a block's
+    // channels are whole 16-byte chunks
+    const int C = C0 + C1, cg = C / G, VEC = 16 / (int)sizeof(T);
+    int gpb = 1;
+    while (gpb <= 8 && ((gpb * cg) % VEC != 0 || G % gpb != 0)) gpb *= 2;
+    if (gpb <= 8 && gpb * cg <= 256) {
+      ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_fa_kernel") : std::string(), 0.0, s);
+      gn_fa_kernel<T><<<dim3(G / gpb, N), 256, 0, s>>>((const double2*)p0, C0, HW / r0, (const double2*)p1, C1,
+                                                      r1 ? HW / r1 : 0, G, gpb, (double)HW * cg, eps, gamma, beta,
+                                                      (const T*)x0, (const T*)x1, HW, silu, (T*)out);
+      IRX_LAUNCH_CHECK();
+      return;
+    }
+  }
   if (p0) {
     ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_finalize_parts_kernel") : std::string(),
                  0.0, s);
@@ -587,6 +675,7 @@ void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* 
 }
 
 bool g_gn_v2 = true;   // irx_set_option("gn_v2", 0): v1 LDS-atomic stats + separate finalize (A/B)
+int g_gn_fa = 1;       // irx_set_option("gn_fa", 0): small-level GroupNorm as finalize + apply launches (A/B)
 
 size_t gn_ws_bytes(int N, int HW, int G) {
   (void)HW;   // partials for up to kMaxChunks chunks per image (v1 and v3 layouts), (mean, rstd), scale / shift

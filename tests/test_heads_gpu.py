@@ -198,3 +198,28 @@ def test_unet_head_major_operands_bit_exact(device, dtype, res):
             outs.append(unet.forward(xin, torch.full((2,), 481.0, device=device), kv, 77).float().cpu())
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("res", [64, 40])
+def test_unet_fused_small_level_groupnorm_bit_exact(device, dtype, res):
+    """GroupNorm at the small levels (HW <= 256: 16^2 / 8^2 at res 64, 10^2 / 5^2 at res 40) as one finalize + apply
+    launch (gn_fa_kernel, option gn_fa, default) vs gn_finalize_parts + gn_apply: the same fold (gn_parts_fold), the
+    same scale / shift and the same per-element op — identical UNet output bit for bit."""
+    from tests import models_common as MC
+    from image_restoration_and_enhancement_amd.engine import UNet
+    pc, sd = MC.state_dicts("denoise")
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    unet = UNet(pc.unet, dtype, device)
+    unet.load_state_dict(sd["unet"])
+    g = torch.Generator().manual_seed(14)
+    xin = torch.zeros(2, res, res, unet.cin_pad)
+    xin[..., :4] = torch.randn(2, res, res, 4, generator=g)
+    xin = xin.to(tdt).to(device).contiguous()
+    kv = unet.prepare_context(torch.randn(2, 77, 768, generator=g).to(tdt).to(device).contiguous())
+    outs = []
+    for v in (1, 0):
+        with L.option(gn_fa=v):
+            outs.append(unet.forward(xin, torch.full((2,), 481.0, device=device), kv, 77).float().cpu())
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
