@@ -534,7 +534,7 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
           const float* beta, int silu, void* out, void* ws, hipStream_t s, const double* p0 = nullptr, int r0 = 0,
           const double* p1 = nullptr, int r1 = 0) {
   float2* ab = gn_ab_ws(ws, N, G);
-  if (p0 && g_gn_fa && HW <= 256) {
+  if (p0 && g_gn_fa && HW <= (g_gn_fa == 1 ? 256 : g_gn_fa)) {
     // small levels: statistics + application in one launch (gn_fa_kernel); GPB groups per block so that a block's
     // channels are whole 16-byte chunks
     const int C = C0 + C1, cg = C / G, VEC = 16 / (int)sizeof(T);
@@ -675,7 +675,8 @@ void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* 
 }
 
 bool g_gn_v2 = true;   // irx_set_option("gn_v2", 0): v1 LDS-atomic stats + separate finalize (A/B)
-int g_gn_fa = 1;       // irx_set_option("gn_fa", 0): small-level GroupNorm as finalize + apply launches (A/B)
+int g_gn_fa = 1;       // irx_set_option("gn_fa", 0): small-level GroupNorm as finalize + apply launches (A/B);
+                       // 1: fused at HW <= 256, > 1: fused at HW <= that value
 
 size_t gn_ws_bytes(int N, int HW, int G) {
   (void)HW;   // partials for up to kMaxChunks chunks per image (v1 and v3 layouts), (mean, rstd), scale / shift

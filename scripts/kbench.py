@@ -66,6 +66,8 @@ ATTNS = [  # (label, B, L, Lk, C)
     ("self d80 L1024", 16, 1024, 1024, 640),
     ("self d160 L256", 16, 256, 256, 1280),
     ("cross d40", 16, 4096, 77, 320),
+    ("cross d80", 16, 1024, 77, 640),
+    ("cross d160", 16, 256, 77, 1280),
 ]
 
 
