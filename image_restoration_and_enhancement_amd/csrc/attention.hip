@@ -868,308 +868,6 @@ __global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// attn3pp: the d = 40 self-attention as a two-group ping-pong (the halo conv's schedule applied to attention).
-// Block = 8 waves, two per SIMD (waves w and w + 4); group A = waves 0-3, group B = waves 4-7; each wave owns QG
-// groups of 32 queries (QG = 2 shares every K / V^T fragment read between them, as attn3q does).  Per 64-key tile j
-// each wave runs an MFMA phase M(j) = [O^T += V_{j-1}^T P_{j-1}^T, S_j^T = K_j Q^T - m] and a VALU phase V(j) = [row
-// max, deferred rescale, p = exp2(S_j), convert -> P_j]; the groups run one phase apart, so in every interval
-// between barriers one wave of a SIMD issues MFMAs while its partner issues the softmax's VALU work (attn3 / attn3q
-// leave that overlap to the hardware scheduler: MFMA busy 0.47, profiles/r05_pmc_top.json).  Phases are pinned by
-// sched_barrier.  K / V tiles live in two LDS stages each; only the VALU-phase group writes LDS: B stages K_{j+1} in
-// phase 2j, A stages V_j in phase 2j + 1, each from registers loaded two phases earlier.  Per 32-query group and
-// tile the arithmetic is attn3's, operation for operation (same MFMA order per accumulator, the deferred max over
-// the group's 32 queries), so the output is bit-identical to attn3 / attn3q.  PRIO: group B (the younger half) at
-// s_setprio 1 for the whole loop (MI355X_MICROARCH.md, two waves per SIMD, item 4).  DBG: timing knock-outs for the
-// per-phase cost model (results wrong): 1 exp2 -> multiply, 2 no row max (the deferred-max check sees 0), 4 no K / V
-// staging (global loads and LDS writes skipped).  Measured (profiles/r05_attn_pp.txt): each removes 6 / 7 / 35 % of
-// the time, but the staging knock-out's gain is the clock's, not the loads': the same loads moved by LDS-DMA up to
-// 3 tiles ahead (no VGPR round trip, no LDS writes) run no faster, and an MFMA fed constant tiles draws less power.
-template <typename T, int D, int KT, int QG, bool PRIO, int DBG = 0>
-__global__ __launch_bounds__(512, 1) void attn3pp_kernel(AttnArgs a) {
-  constexpr int QB = 8 * 32 * QG;                          // queries per block
-  constexpr int DQ = (D + 15) / 16 * 16, NS = DQ / 16;
-  constexpr int NDT = (D + 31) / 32;
-  constexpr bool ONES = D % 32 != 0;
-  constexpr int DVP = NDT * 32;
-  constexpr int SK = ((DQ / 8) % 2 == 0) ? DQ + 8 : DQ;
-  constexpr int SV = (DVP % 128 == 32 || DVP % 128 == 96) ? DVP : DVP + 32;
-  constexpr int NSUB = KT / 32;
-  constexpr int CPR = D / 8;
-  constexpr int NCH = (KT * CPR + 255) / 256;              // staging slots per thread of a group (256 threads)
-  constexpr float THR = 8.f;
-  constexpr bool PADM = DQ > D;
-  static_assert(D % 8 == 0 && KT % 32 == 0 && PADM && ONES, "attn3pp: the d = 40 shape");
-  __shared__ __attribute__((aligned(16))) uint16_t Ks2[2 * KT * SK];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs2[2 * KT * SV];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2);   // 0: group A, 1: group B
-  const int gt = tid & 255;                                     // thread index within the group
-  const int r = lane & 31, hh = lane >> 5, g = lane >> 4;
-  const int nq = (a.Lq + QB - 1) / QB;
-  const int nblk = nq * a.H * a.B;
-  const int lid = a.xcd ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
-  const int qb = lid % nq, bh = lid / nq;
-  const int b = bh / a.H, h = bh - b * a.H;
-  const T* __restrict__ Q = (const T*)a.q + (long)b * a.sq + (long)h * (a.hsq ? a.hsq : D);
-  const T* __restrict__ K = (const T*)a.k + (long)b * a.sk + (long)h * (a.hsk ? a.hsk : D);
-  const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : D);
-
-  // pad columns: K[.][d] = 1 (carries -m from Q), K[.][d + 1] = the key mask (neg_big past Lk, Q[d + 1] = 1),
-  // V[.][d] = 1 (the row sums)
-  for (int i = tid; i < 2 * KT * SK; i += 512) Ks2[i] = (i % SK == D) ? one_bits<T>() : (uint16_t)0;
-  for (int i = tid; i < 2 * KT * SV; i += 512) Vs2[i] = (i % SV == D) ? one_bits<T>() : (uint16_t)0;
-
-  // staging: group B moves K tiles, group A V tiles; slot u of thread gt = (row, 16-byte chunk) of the tile
-  const T* src = grp ? K : V;
-  const long ld = grp ? a.ldk : a.ldv;
-  const int SS = grp ? SK : SV;
-  uint16_t* const dst2 = grp ? Ks2 : Vs2;
-  uint4 sreg[NCH];
-  int srow[NCH], soff[NCH];
-  const T* sp[NCH];
-#pragma unroll
-  for (int u = 0; u < NCH; ++u) {
-    const int idx = min(gt + 256 * u, KT * CPR - 1);
-    const int row = idx / CPR, c = idx - row * CPR;
-    srow[u] = row;
-    sp[u] = src + (long)row * ld + c * 8;
-    soff[u] = row * SS + c * 8;
-  }
-  auto slot_ok = [&](int u) { return u < NCH - 1 || gt + 256 * u < KT * CPR; };
-  auto gload = [&](int j0) {   // this group's operand of the tile at key j0 -> registers
-    if constexpr ((DBG & 4) != 0) return;
-    const long o = (long)j0 * ld;
-#pragma unroll
-    for (int u = 0; u < NCH; ++u) {
-      const bool in = slot_ok(u) && j0 + srow[u] < a.Lk;
-      sreg[u] = in ? *(const uint4*)(sp[u] + o) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto lstage = [&](int buf, int j0) {   // registers -> LDS stage buf (+ the key mask of a ragged K tile)
-    if constexpr ((DBG & 4) != 0) return;
-#pragma unroll
-    for (int u = 0; u < NCH; ++u)
-      if (slot_ok(u)) *(uint4*)(dst2 + buf * KT * SS + soff[u]) = sreg[u];
-    if (grp && j0 + KT > a.Lk && gt < KT && j0 + gt >= a.Lk) Ks2[buf * KT * SK + gt * SK + D + 1] = neg_big_bits<T>();
-  };
-
-  const int q0 = qb * QB + wave * 32 * QG;
-  uint4 qf[QG][NS];
-  const float sl2 = a.scale * 1.4426950408889634f;
-#pragma unroll
-  for (int gq = 0; gq < QG; ++gq) {
-    const int qrow = q0 + 32 * gq + r;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int e = 16 * s + 8 * hh;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (qrow < a.Lq && e < D) v = *(const uint4*)(Q + (long)qrow * a.ldq + e);
-      if (!a.q_scaled) {
-        float f[8];
-        Vec16<T>::unpack(v, f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] *= sl2;
-        v = Vec16<T>::pack(f);
-      }
-      if (e == D) v.x = (uint32_t)one_bits<T>() << 16;   // Q[d + 1] = 1: the key-mask column
-      qf[gq][s] = v;
-    }
-  }
-  constexpr int PADS = D / 16;
-  f32x16 oacc[QG][NDT], sacc[QG][NSUB];
-#pragma unroll
-  for (int gq = 0; gq < QG; ++gq)
-#pragma unroll
-    for (int i = 0; i < NDT; ++i)
-#pragma unroll
-      for (int k = 0; k < 16; ++k) oacc[gq][i][k] = 0.f;
-  uint4 pb[QG][NSUB][2];
-  float m[QG];
-#pragma unroll
-  for (int gq = 0; gq < QG; ++gq) m[gq] = 0.f;
-  const int nt = (a.Lk + KT - 1) / KT;
-
-  auto barrier = [] {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // O^T += V_j^T P_j^T (V_j in stage j & 1), every query group from one V^T fragment read
-  auto pv = [&](int j) {
-    const uint16_t* Vs = Vs2 + (j & 1) * KT * SV;
-    uint4 vf[NSUB][NDT][2];
-#pragma unroll
-    for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int krow = 32 * c + 16 * s2 + 4 * (g >> 1) + ((lane & 15) >> 2);
-          const int col = 32 * dt + 16 * (g & 1) + 4 * (lane & 3);
-          const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + krow * SV + col));
-          const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vs + (krow + 8) * SV + col));
-          vf[c][dt][s2] = make_uint4(__builtin_bit_cast(uint2, t1).x, __builtin_bit_cast(uint2, t1).y,
-                                     __builtin_bit_cast(uint2, t2).x, __builtin_bit_cast(uint2, t2).y);
-        }
-#pragma unroll
-    for (int gq = 0; gq < QG; ++gq)
-#pragma unroll
-      for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-            oacc[gq][dt] = Mfma<T>::m32x32x16(vf[c][dt][s2], pb[gq][c][s2], oacc[gq][dt]);
-  };
-  // S_j^T = K_j Q^T - m (K_j in stage j & 1)
-  auto qk = [&](int j) {
-    const uint16_t* Ks = Ks2 + (j & 1) * KT * SK;
-    uint4 kf[NS][NSUB];
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-#pragma unroll
-      for (int c = 0; c < NSUB; ++c) kf[s][c] = *(const uint4*)(Ks + (c * 32 + r) * SK + 16 * s + 8 * hh);
-#pragma unroll
-    for (int gq = 0; gq < QG; ++gq)
-#pragma unroll
-      for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-        for (int k = 0; k < 16; ++k) sacc[gq][c][k] = 0.f;
-#pragma unroll
-    for (int gq = 0; gq < QG; ++gq)
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int c = 0; c < NSUB; ++c) sacc[gq][c] = Mfma<T>::m32x32x16(kf[s][c], qf[gq][s], sacc[gq][c]);
-  };
-  // VALU phase of a tile: per query group row max, deferred rescale, P = exp2(S) in the storage type
-  auto vphase = [&](bool first) {
-#pragma unroll
-    for (int gq = 0; gq < QG; ++gq) {
-      float mx[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) mx[t] = fmaxf(sacc[gq][0][4 * t], sacc[gq][0][4 * t + 1]);
-#pragma unroll
-      for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int k = (c == 0 ? 2 : 0); k < 4; k += 2)
-            mx[t] = fmaxf(fmaxf(mx[t], sacc[gq][c][4 * t + k]), sacc[gq][c][4 * t + k + 1]);
-      float tmax = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
-      tmax = fmaxf(tmax, xlane32(tmax));
-      if constexpr (DBG & 2) tmax = 0.f;
-      if (first || __any(tmax > THR)) {
-        const float tgt = first ? (tmax == -INFINITY ? 0.f : m[gq] + tmax) : m[gq] + fmaxf(tmax, 0.f);
-        const float mn = Mfma<T>::round(tgt);
-        const float delta = mn - m[gq];
-        const float alpha = __builtin_amdgcn_exp2f(-delta);
-#pragma unroll
-        for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-          for (int k = 0; k < 16; ++k) sacc[gq][c][k] -= delta;
-        if (!first) {
-#pragma unroll
-          for (int i = 0; i < NDT; ++i)
-#pragma unroll
-            for (int k = 0; k < 16; ++k) oacc[gq][i][k] *= alpha;
-        }
-        m[gq] = mn;
-        if (hh) qf[gq][PADS].x = (qf[gq][PADS].x & 0xFFFF0000u) | (Mfma<T>::pack2(-mn, 0.f) & 0xFFFFu);
-      }
-#pragma unroll
-      for (int c = 0; c < NSUB; ++c)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          float p[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            p[j] = (DBG & 1) ? sacc[gq][c][8 * s2 + j] * 0.5f : __builtin_amdgcn_exp2f(sacc[gq][c][8 * s2 + j]);
-          pb[gq][c][s2] = make_uint4(Mfma<T>::pack2(p[0], p[1]), Mfma<T>::pack2(p[2], p[3]),
-                                     Mfma<T>::pack2(p[4], p[5]), Mfma<T>::pack2(p[6], p[7]));
-        }
-    }
-  };
-
-  // Phase p (between consecutive barriers): A runs M(p/2) on even p and V(p/2) on odd p, B runs V(p/2 - 1) on even
-  // p and M(p/2) on odd p, where M(j) = [PV_{j-1}, QK_j] and V(j) = softmax of tile j.  B stages K_{j+1} in phase 2j,
-  // A stages V_j in phase 2j + 1, each from registers loaded two phases earlier (a load past Lk reads nothing and
-  // stages zeros into a stage no later phase reads).  Each group runs its own straight-line loop (no per-phase role
-  // branches, so no register moves and no wait on the just-issued loads at the loop edge); both pass 2 nt + 1
-  // barriers.
-  if (grp) gload(0);
-  __syncthreads();          // pad columns initialised
-  if (grp == 0) {
-    gload(0);
-    __syncthreads();
-    qk(0);                                             // phase 0
-    barrier();
-    vphase(true);                                      // phase 1
-    lstage(0, 0);
-    gload(KT);
-    barrier();
-    for (int j = 1; j < nt; ++j) {
-      pv(j - 1);                                       // phase 2j
-      qk(j);
-      barrier();
-      vphase(false);                                   // phase 2j + 1
-      lstage(j & 1, j * KT);
-      gload((j + 1) * KT);
-      barrier();
-    }
-    pv(nt - 1);                                        // phase 2 nt
-    barrier();
-  } else {
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-    lstage(0, 0);
-    gload(KT);
-    __syncthreads();
-    lstage(1, KT);                                     // phase 0
-    gload(2 * KT);
-    barrier();
-    qk(0);                                             // phase 1
-    barrier();
-    for (int j = 1; j < nt; ++j) {
-      vphase(j == 1);                                  // phase 2j
-      lstage((j + 1) & 1, (j + 1) * KT);
-      gload((j + 2) * KT);
-      barrier();
-      pv(j - 1);                                       // phase 2j + 1
-      qk(j);
-      barrier();
-    }
-    vphase(nt == 1);                                   // phase 2 nt
-    barrier();
-    pv(nt - 1);                                        // phase 2 nt + 1
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-  }
-
-  // ---- normalise (row sums from the ones column of V), store O[q][h*d + e]
-  constexpr int dts = D / 32, rho = D % 32, hs = (rho >> 2) & 1, reg = (rho & 3) + 4 * (rho >> 3);
-#pragma unroll
-  for (int gq = 0; gq < QG; ++gq) {
-    const int qrow = q0 + 32 * gq + r;
-    const float v = oacc[gq][dts][reg];
-    const float o = xlane32(v);
-    const float l = hh == hs ? v : o;
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    if (qrow < a.Lq) {
-      T* __restrict__ O = (T*)a.o + (long)b * a.so + (long)h * (a.hso ? a.hso : D) + (long)qrow * a.ldo;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int e = 32 * dt + 8 * k + 4 * hh;
-          if (e >= D) continue;
-          *(uint2*)(O + e) = make_uint2(Mfma<T>::pack2(oacc[gq][dt][4 * k] * inv, oacc[gq][dt][4 * k + 1] * inv),
-                                        Mfma<T>::pack2(oacc[gq][dt][4 * k + 2] * inv, oacc[gq][dt][4 * k + 3] * inv));
-        }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // attnw: flash attention for wide heads (the VAE mid-block's single d = 512 head), bf16 / fp16, non-causal.
 // Block = 4 waves x the same 32 queries; wave w owns d-quarter w.  Per 32-key tile:
 //   partial S^T_w = K[:, d_w] Q[:, d_w]^T (D/64 k-steps of v_mfma_f32_32x32x16, K fragments straight from
@@ -1338,20 +1036,15 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
   dim3 grid(nq * a.H * a.B), block(256);
   // which kernel runs: resident K/V (cross-attention), two query groups per wave (d = 40 self), the prefetching
   // attn3 (PF 3), or plain attn3; the profiler names the launch as rocprofv3 demangles it
-  enum { kRes, kPP, kQ2, kPf, kPlain };
+  enum { kRes, kQ2, kPf, kPlain };
   int kind = kPlain;
   if (!CAUSAL && res) kind = kRes;
-  else if (!CAUSAL && D == 40 && g_attn_pp) kind = kPP;
   else if (!CAUSAL && D == 40 && g_attn_q2) kind = kQ2;
   else if (!CAUSAL && D == 40 && g_attn_pf) kind = kPf;
   std::string nm;
   if (prof_on()) {
     const std::string tn = std::is_same<T, f16_t>::value ? "_Float16" : "unsigned short";
-    nm = kind == kPP ? "irx::(anonymous namespace)::attn3pp_kernel<" + tn + ", " + std::to_string(D) + ", " +
-                           std::to_string(KT) + ", " + ((g_attn_pp & 3) == 2 ? "2" : "1") + ", " +
-                           (g_attn_pp & 4 ? "true" : "false") +
-                           (g_attn_pp > 7 ? ", " + std::to_string(g_attn_pp >> 3) : std::string()) + ">"
-       : kind == kQ2 ? "irx::(anonymous namespace)::attn3q_kernel<" + tn + ", " + std::to_string(D) + ", " +
+    nm = kind == kQ2 ? "irx::(anonymous namespace)::attn3q_kernel<" + tn + ", " + std::to_string(D) + ", " +
                            std::to_string(KT) + ">"
                      : "irx::(anonymous namespace)::attn3_kernel<" + tn + ", " + std::to_string(D) + ", " +
                            std::to_string(KT) + ", " + (CAUSAL ? "true" : "false") + ", " +
@@ -1371,22 +1064,6 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
       return;
     }
     if constexpr (D == 40) {
-      if (kind == kPP) {   // attn_pp: 1 one query group per wave, 2 two; | 4: group B at priority 1; | 8, 16, 32:
-                           // timing knock-outs (results wrong; with 5 only): exp2, row max, staging
-        const int qg = (g_attn_pp & 3) == 2 ? 2 : 1;
-        const dim3 gpp(((a.Lq + 256 * qg - 1) / (256 * qg)) * a.H * a.B), bpp(512);
-        switch (g_attn_pp) {
-          case 2: attn3pp_kernel<T, D, KT, 2, false><<<gpp, bpp, 0, s>>>(b); break;
-          case 6: attn3pp_kernel<T, D, KT, 2, true><<<gpp, bpp, 0, s>>>(b); break;
-          case 5: attn3pp_kernel<T, D, KT, 1, true><<<gpp, bpp, 0, s>>>(b); break;
-          case 5 | 8: attn3pp_kernel<T, D, KT, 1, true, 1><<<gpp, bpp, 0, s>>>(b); break;
-          case 5 | 16: attn3pp_kernel<T, D, KT, 1, true, 2><<<gpp, bpp, 0, s>>>(b); break;
-          case 5 | 32: attn3pp_kernel<T, D, KT, 1, true, 4><<<gpp, bpp, 0, s>>>(b); break;
-          default: attn3pp_kernel<T, D, KT, 1, false><<<gpp, bpp, 0, s>>>(b); break;
-        }
-        IRX_LAUNCH_CHECK();
-        return;
-      }
       if (kind == kQ2) {
         attn3q_kernel<T, D, KT><<<dim3(((a.Lq + 255) / 256) * a.H * a.B), block, 0, s>>>(b);
         IRX_LAUNCH_CHECK();
@@ -1463,8 +1140,6 @@ void attention(const AttnArgs& a, hipStream_t s) {
     launch_t<bf16_t>(a, s);
   }
 }
-int g_attn_pp = 0;     // d = 40 self-attention: 0 attn3q / attn3; 1, 2, 5, 6 attn3pp (see the launch; A/B: faster alone,
-                       // 3.5 % slower inside the UNet step, profiles/r05_attn_pp.txt)
 int g_attn_q2 = 1;     // irx_set_option("attn_q2", 0): d = 40 self-attention with one query group per wave (attn3, A/B)
 int g_attn_pf = 1;     // irx_set_option("attn_pf", 0): d = 40 self-attention without the whole-tile fragment prefetch (A/B)
 int g_attn_xcd = 1;

@@ -79,7 +79,6 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gn_narrow", &g_gn_narrow, nullptr},
     {"attn_pf", &g_attn_pf, nullptr},
     {"attn_q2", &g_attn_q2, nullptr},
-    {"attn_pp", &g_attn_pp, nullptr},
     {"conv1x1_dense", &g_conv1x1_dense, nullptr},
     {"gn_fa", &g_gn_fa, nullptr},
     {"halo_split", &g_halo_split, nullptr},

@@ -242,7 +242,6 @@ struct AttnArgs {
   int qrep = 1;           // (set by the launcher) query groups per block over resident K/V
 };
 void attention(const AttnArgs& a, hipStream_t s);
-extern int g_attn_pp;    // non-causal streamed d = 40 attention as the two-group MFMA / softmax ping-pong (attn3pp): 0 off
 extern int g_attn_q2;    // 1: non-causal streamed d = 40 attention with two 32-query groups per wave (attn3q)
 extern int g_attn_pf;    // 1: non-causal streamed d = 40 attention with whole-tile K / V fragment prefetch (attn3 PF)
 extern int g_attn_prio;

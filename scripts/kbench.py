@@ -91,9 +91,6 @@ def main():
     ap.add_argument("--match", default="", help="only shapes whose label contains this")
     ap.add_argument("--ref", action="store_true", help="also time torch (hipBLASLt / MIOpen) on the same shapes")
     ap.add_argument("--variants", default="s2,ring64,small")
-    ap.add_argument("--attn-ko", type=lambda t: [int(x) for x in t.split(",")], default=[],
-                    help="attn3pp timing knock-outs to time beside the variants (results wrong): 8 exp2, 16 row "
-                         "max, 32 staging")
     args = ap.parse_args()
     dev = torch.device("cuda")
     L.load()
@@ -167,11 +164,7 @@ def main():
             v = torch.randn(B, Lk, C, device=dev, generator=g).to(dt)
             flops = 4.0 * B * Lq * Lk * C
             res = []
-            for vn, opts in (("pf", {"attn_pf": 1, "attn_q2": 0, "attn_pp": 0}),
-                             ("q2", {"attn_pf": 1, "attn_q2": 1, "attn_pp": 0}),
-                             ("pp", {"attn_pp": 1}), ("pp_q2", {"attn_pp": 2}), ("pp_prio", {"attn_pp": 5}),
-                             ("pp_q2_prio", {"attn_pp": 6})) + tuple(
-                                 (f"ko{k}", {"attn_pp": 5 | k}) for k in args.attn_ko):
+            for vn, opts in (("pf", {"attn_pf": 1, "attn_q2": 0}), ("q2", {"attn_pf": 1, "attn_q2": 1})):
                 with L.option(**opts):
                     ms = timeit(lambda: O.attention(q, k, v, 8), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")

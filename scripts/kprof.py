@@ -4,6 +4,7 @@ target a single kernel (`--kernel-include-regex`) without the rest of the bench 
 
   python scripts/kprof.py --op conv320      halo 3x3 conv, 64x64 level, 320 -> 320
   python scripts/kprof.py --op geglu320     GEGLU feed-forward projection, M 65536, K 320, N 2560
+  python scripts/kprof.py --op geglu640     ... 32^2 level (M 16384, K 640); geglu1280: 16^2 (M 4096, K 1280)
   python scripts/kprof.py --op lin320       K = 320 projection (proj_in / to_q), M 65536, N 320
   python scripts/kprof.py --op lin320r      ... + residual (to_out / proj_out)
   python scripts/kprof.py --op qkv320       q|k|v projection, N 960 (row-major here)
@@ -47,8 +48,9 @@ def main():
         x, w = rn(16, 64, 64, 320), rn(320, 320, 3, 3, scale=1 / math.sqrt(2880)).float()
         b = torch.zeros(320, device=dev)
         fn = lambda: O.conv2d(x, w, b)                                       # noqa: E731
-    elif a.op in ("geglu320",):
-        C, M = 320, 65536
+    elif a.op in ("geglu320", "geglu640", "geglu1280"):
+        C = int(a.op[5:])
+        M = {320: 65536, 640: 16384, 1280: 4096}[C]
         A, Wt = rn(M, C), rn(8 * C, C, scale=1 / math.sqrt(C))[geglu64_order(8 * C)].contiguous()
         bias = torch.zeros(8 * C, device=dev)
         out = torch.empty(M, 4 * C, dtype=dt, device=dev)

@@ -698,9 +698,9 @@ def test_attention_prefetch_d40_bit_exact(device, dt, B, Lq, Lk):
     C, heads = 320, 8
     q, k, v = _r(B, Lq, C, seed=73) * 2, _r(B, Lk, C, seed=74) * 2, _r(B, Lk, C, seed=75)
     qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
-    with L.option(attn_pp=0, attn_pf=1, attn_q2=0):
+    with L.option(attn_pf=1, attn_q2=0):
         got = O.attention(qd, kd, vd, heads)
-    with L.option(attn_pp=0, attn_pf=0, attn_q2=0):
+    with L.option(attn_pf=0, attn_q2=0):
         base = O.attention(qd, kd, vd, heads)
     torch.cuda.synchronize()
     assert torch.equal(got, base)
@@ -716,29 +716,9 @@ def test_attention_two_query_groups_d40_bit_exact(device, dt, B, Lq, Lk):
     C, heads = 320, 8
     q, k, v = _r(B, Lq, C, seed=76) * 2, _r(B, Lk, C, seed=77) * 2, _r(B, Lk, C, seed=78)
     qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
-    with L.option(attn_pp=0, attn_q2=1):
+    with L.option(attn_q2=1):
         got = O.attention(qd, kd, vd, heads)
-    with L.option(attn_pp=0, attn_q2=0, attn_pf=0):
-        base = O.attention(qd, kd, vd, heads)
-    torch.cuda.synchronize()
-    assert torch.equal(got, base)
-
-
-@pytest.mark.parametrize("dt", DT16)
-@pytest.mark.parametrize("pp", [1, 2, 5, 6])
-@pytest.mark.parametrize("B,Lq,Lk", [(2, 1024, 1024), (1, 333, 190), (1, 64, 129), (1, 300, 64), (2, 4096, 4096)])
-def test_attention_ping_pong_d40_bit_exact(device, dt, pp, B, Lq, Lk):
-    """attn3pp (option attn_pp: 8 waves, two groups of 4 offset by half a key tile so one group's QK / PV MFMAs run
-    while the other's softmax runs; each wave computes the same 2 x 32 queries with the same per-tile arithmetic as
-    attn3q; pp 2: two query groups per wave; | 4: group B at priority 1): identical outputs bit for bit, ragged query
-    and key counts and a single key tile included."""
-    from image_restoration_and_enhancement_amd import _lib as L
-    C, heads = 320, 8
-    q, k, v = _r(B, Lq, C, seed=86) * 2, _r(B, Lk, C, seed=87) * 2, _r(B, Lk, C, seed=88)
-    qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
-    with L.option(attn_pp=pp):
-        got = O.attention(qd, kd, vd, heads)
-    with L.option(attn_pp=0, attn_q2=1):
+    with L.option(attn_q2=0, attn_pf=0):
         base = O.attention(qd, kd, vd, heads)
     torch.cuda.synchronize()
     assert torch.equal(got, base)
