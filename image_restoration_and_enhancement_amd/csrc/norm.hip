@@ -290,25 +290,40 @@ __global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const double2* _
   }
 }
 
-// GroupNorm from producer partials, statistics and application in ONE launch for the small levels (HW <= 256: the
-// UNet's 16^2 / 8^2 tensors, option gn_fa): block = (image n, GPB consecutive groups); its lanes fold the groups'
-// partials exactly as gn_finalize_parts_kernel does (gn_parts_fold), the channels' scale / shift go to LDS, then
-// the block applies them (gn_act, as gn_apply_kernel) to its channels of every pixel, 16-byte chunks, four loads in
-// flight per thread.  Bit-identical to gn_finalize_parts_kernel + gn_apply_kernel; one launch and one tiny kernel's
-// ramp / drain fewer per GroupNorm.
+// GroupNorm from producer partials, statistics and application in ONE launch (option gn_fa): block = (image n,
+// GPB consecutive groups, pixel slice); its lanes fold the groups' partials exactly as gn_finalize_parts_kernel does
+// (gn_parts_fold), the channels' scale / shift go to LDS, then the block applies them (gn_act, as gn_apply_kernel) to
+// its channels of the slice's pixels, 16-byte chunks, four loads in flight per thread.  Bit-identical to
+// gn_finalize_parts_kernel + gn_apply_kernel; one launch and one tiny kernel's ramp / drain fewer per GroupNorm.  The
+// S slices of an image re-fold the same partials (a few KiB from L2 per block).  1-D grid of G / GPB x N x S blocks;
+// xmap (host: N * S % 8 == 0): the G / GPB blocks of one (image, slice) are consecutive blocks of ONE XCD (blocks
+// are dealt to the 8 XCDs round-robin), so the 16-byte pieces of a pixel's channels meet in one L2.
 template <typename T>
 __global__ __launch_bounds__(256) void gn_fa_kernel(const double2* __restrict__ p0, int C0, int rpi0,
                                                     const double2* __restrict__ p1, int C1, int rpi1, int G, int gpb,
                                                     double cnt, float eps, const float* __restrict__ gamma,
                                                     const float* __restrict__ beta, const T* __restrict__ x0,
-                                                    const T* __restrict__ x1, int HW, int silu, T* __restrict__ out) {
+                                                    const T* __restrict__ x1, int HW, int S, int xmap, int silu,
+                                                    T* __restrict__ out) {
   constexpr int VEC = 16 / (int)sizeof(T);
   __shared__ float2 gmr[8];
   __shared__ float2 sab[256];
-  const int n = blockIdx.y, t = threadIdx.x;
+  const int ngb = G / gpb, L = blockIdx.x;
+  int gb, u;
+  if (xmap) {
+    const int j = L >> 3;
+    gb = j % ngb;
+    u = (j / ngb) * 8 + (L & 7);
+  } else {
+    gb = L % ngb;
+    u = L / ngb;
+  }
+  const int n = u / S, sl = u - n * S;
+  const int hws = (HW + S - 1) / S, plo = sl * hws, np = max(0, min(HW, plo + hws) - plo);
+  const int t = threadIdx.x;
   const int C = C0 + C1, cg = C / G;
-  const int gl = t >> 5, sub = t & 31, g = blockIdx.x * gpb + gl;
-  const int c0 = blockIdx.x * gpb * cg, nc = gpb * cg;
+  const int gl = t >> 5, sub = t & 31, g = gb * gpb + gl;
+  const int c0 = gb * gpb * cg, nc = gpb * cg;
   const float gam = t < nc ? gamma[c0 + t] : 0.f, bet = t < nc ? beta[c0 + t] : 0.f;
   const float2 r = gn_parts_fold(p0, C0, rpi0, p1, C1, rpi1, n, g, gl < gpb, cg, sub, cnt, eps);
   if (sub == 0 && gl < gpb) gmr[gl] = r;
@@ -319,10 +334,10 @@ __global__ __launch_bounds__(256) void gn_fa_kernel(const double2* __restrict__ 
     sab[t] = make_float2(sc, fmaf(-q.x, sc, bet));
   }
   __syncthreads();
-  const int nch = nc / VEC, tot = HW * nch;
+  const int nch = nc / VEC, tot = np * nch;
   auto src_of = [&](int idx, int& k) -> const T* {
-    const int p = idx / nch;
-    k = idx - p * nch;
+    const int pp = idx / nch, p = plo + pp;
+    k = idx - pp * nch;
     const int c = c0 + k * VEC;
     return c < C0 ? x0 + ((long)n * HW + p) * C0 + c : x1 + ((long)n * HW + p) * C1 + (c - C0);
   };
@@ -334,7 +349,7 @@ __global__ __launch_bounds__(256) void gn_fa_kernel(const double2* __restrict__ 
       const float2 q = sab[k * VEC + e];
       f[e] = gn_act(f[e], q.x, q.y, silu);
     }
-    const int p = idx / nch;
+    const int p = plo + idx / nch;
     *(uint4*)(out + ((long)n * HW + p) * C + c0 + k * VEC) = Vec16<T>::pack(f);
   };
   int idx = t;
@@ -535,16 +550,28 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
           const double* p1 = nullptr, int r1 = 0) {
   float2* ab = gn_ab_ws(ws, N, G);
   if (p0 && g_gn_fa && HW <= (g_gn_fa == 1 ? 256 : g_gn_fa)) {
-    // small levels: statistics + application in one launch (gn_fa_kernel); GPB groups per block so that a block's
-    // channels are whole 16-byte chunks
+    // statistics + application in one launch (gn_fa_kernel); GPB groups per block so that a block's channels are
+    // whole 16-byte chunks.  Small levels (HW <= 256): one block per (image, GPB groups); larger ones (gn_fa = an
+    // HW bound > 256) split each image's pixels into S slices, S so that the grid has ~2048 blocks
     const int C = C0 + C1, cg = C / G, VEC = 16 / (int)sizeof(T);
     int gpb = 1;
     while (gpb <= 8 && ((gpb * cg) % VEC != 0 || G % gpb != 0)) gpb *= 2;
     if (gpb <= 8 && gpb * cg <= 256) {
+      if (HW > 256 && g_gn_fa_wide) {   // sliced levels: the widest valid channel span (longer 16-byte runs per pixel)
+        for (int q = gpb * 2; q <= 8 && G % q == 0 && q * cg <= 256; q *= 2) gpb = q;
+      }
+      const long base = (long)(G / gpb) * N;
+      int S = 1;
+      if (HW > 256) {
+        const long want = 2048;
+        while ((long)S * 2 * base <= want && HW / (S * 2) >= 64) S *= 2;
+      }
+      const int xmap = ((long)N * S) % 8 == 0;
       ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::gn_fa_kernel") : std::string(), 0.0, s);
-      gn_fa_kernel<T><<<dim3(G / gpb, N), 256, 0, s>>>((const double2*)p0, C0, HW / r0, (const double2*)p1, C1,
-                                                      r1 ? HW / r1 : 0, G, gpb, (double)HW * cg, eps, gamma, beta,
-                                                      (const T*)x0, (const T*)x1, HW, silu, (T*)out);
+      gn_fa_kernel<T><<<dim3((unsigned)(base * S)), 256, 0, s>>>((const double2*)p0, C0, HW / r0, (const double2*)p1,
+                                                                 C1, r1 ? HW / r1 : 0, G, gpb, (double)HW * cg, eps,
+                                                                 gamma, beta, (const T*)x0, (const T*)x1, HW, S, xmap,
+                                                                 silu, (T*)out);
       IRX_LAUNCH_CHECK();
       return;
     }
@@ -675,8 +702,11 @@ void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* 
 }
 
 bool g_gn_v2 = true;   // irx_set_option("gn_v2", 0): v1 LDS-atomic stats + separate finalize (A/B)
-int g_gn_fa = 1;       // irx_set_option("gn_fa", 0): small-level GroupNorm as finalize + apply launches (A/B);
-                       // 1: fused at HW <= 256, > 1: fused at HW <= that value
+int g_gn_fa_wide = 1;  // irx_set_option("gn_fa_wide", 0): sliced gn_fa blocks over the fewest groups (A/B)
+int g_gn_fa = 4096;    // irx_set_option("gn_fa", 0): GroupNorm from partials as finalize + apply launches (A/B);
+                       // 1: one fused launch at HW <= 256; > 1: at HW <= that value (pixel slices above 256).
+                       // 4096 (the UNet's 64^2 level and below): -1.5 ms/step of norm kernels vs 1
+                       // (profiles/r05_bench_gn_fa_slices.txt); the 512^2 VAE's wider levels keep two launches
 
 size_t gn_ws_bytes(int N, int HW, int G) {
   (void)HW;   // partials for up to kMaxChunks chunks per image (v1 and v3 layouts), (mean, rstd), scale / shift

@@ -185,7 +185,8 @@ extern int g_conv_halo;      // 3x3 convs on whole-row tiles: one LDS halo per 3
 extern int g_gemm_pp;        // 1: ping-pong main loop for dense GEMMs (off: measured slower, see gemm2.hip)
 extern int g_halo_pipe;      // 1: software-pipelined halo main loop (fragments read one sub-step ahead)
 extern int g_halo_split;     // halo convs whose tiles alone do not fill the chip take two K splits
-extern int g_gn_fa;        // GroupNorm from partials at HW <= 256: one fused finalize + apply launch (gn_fa_kernel)
+extern int g_gn_fa;        // GroupNorm from partials as one fused finalize + apply launch (gn_fa_kernel) at HW <= g_gn_fa
+extern int g_gn_fa_wide;
 extern bool g_gn_v2;       // GroupNorm stats v3 (slabbed grid + finalize kernel); 0 = v1 (A/B)
 void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
                 const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s);

@@ -218,8 +218,36 @@ def test_unet_fused_small_level_groupnorm_bit_exact(device, dtype, res):
     xin = xin.to(tdt).to(device).contiguous()
     kv = unet.prepare_context(torch.randn(2, 77, 768, generator=g).to(tdt).to(device).contiguous())
     outs = []
-    for v in (1, 0):
-        with L.option(gn_fa=v):
+    # 1: small levels only; 1 << 30: every level (pixel slices above HW 256, XCD-grouped), over the widest / the
+    # narrowest channel span per block; 1024: up to 32^2
+    for v, wide in ((0, 1), (1, 1), (1 << 30, 1), (1 << 30, 0), (1024, 1)):
+        with L.option(gn_fa=v, gn_fa_wide=wide):
             outs.append(unet.forward(xin, torch.full((2,), 481.0, device=device), kv, 77).float().cpu())
     assert torch.isfinite(outs[0]).all()
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_vae_fused_groupnorm_slices_bit_exact(device, dtype):
+    """The VAE's GroupNorms from producer partials (64^2 .. 128^2 levels here, N = 1 and 2) as one sliced finalize +
+    apply launch (gn_fa 1 << 30) vs gn_finalize_parts + gn_apply (gn_fa 0): identical encoder and decoder outputs."""
+    from tests import models_common as MC
+    from image_restoration_and_enhancement_amd.engine import VAE
+    pc, sd = MC.state_dicts("denoise")
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    vae = VAE(pc.vae, dtype, device)
+    vae.load_state_dict(sd["vae"])
+    g = torch.Generator().manual_seed(15)
+    for n in (1, 2):
+        img = torch.zeros(n, 128, 128, 8)
+        img[..., :3] = torch.rand(n, 128, 128, 3, generator=g) * 2 - 1
+        img = img.to(tdt).to(device).contiguous()
+        res = []
+        for v in (0, 1 << 30):
+            with L.option(gn_fa=v):
+                z = vae.encode(img).contiguous()
+                res.append((z.float().cpu(), vae.decode(z).float().cpu()))
+        for k in range(2):
+            assert torch.isfinite(res[1][k]).all()
+            assert torch.equal(res[1][k], res[0][k]), (n, k)
