@@ -82,6 +82,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"conv1x1_dense", &g_conv1x1_dense, nullptr},
     {"gn_fa", &g_gn_fa, nullptr},
     {"gn_fa_wide", &g_gn_fa_wide, nullptr},
+    {"gn_fa_blocks", &g_gn_fa_blocks, nullptr},
     {"halo_split", &g_halo_split, nullptr},
     {"halo_pipe", &g_halo_pipe, nullptr},
     {"gemm_pp", &g_gemm_pp, nullptr},

@@ -563,7 +563,7 @@ void gn_t(const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, 
       const long base = (long)(G / gpb) * N;
       int S = 1;
       if (HW > 256) {
-        const long want = 2048;
+        const long want = g_gn_fa_blocks;
         while ((long)S * 2 * base <= want && HW / (S * 2) >= 64) S *= 2;
       }
       const int xmap = ((long)N * S) % 8 == 0;
@@ -702,6 +702,7 @@ void gn_fold_weights(int dtype, const void* W, const float* bias, const float2* 
 }
 
 bool g_gn_v2 = true;   // irx_set_option("gn_v2", 0): v1 LDS-atomic stats + separate finalize (A/B)
+int g_gn_fa_blocks = 2048;   // irx_set_option("gn_fa_blocks", n): grid size the sliced gn_fa aims at (sweeps)
 int g_gn_fa_wide = 1;  // irx_set_option("gn_fa_wide", 0): sliced gn_fa blocks over the fewest groups (A/B)
 int g_gn_fa = 4096;    // irx_set_option("gn_fa", 0): GroupNorm from partials as finalize + apply launches (A/B);
                        // 1: one fused launch at HW <= 256; > 1: at HW <= that value (pixel slices above 256).

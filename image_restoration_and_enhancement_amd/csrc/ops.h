@@ -187,6 +187,7 @@ extern int g_halo_pipe;      // 1: software-pipelined halo main loop (fragments 
 extern int g_halo_split;     // halo convs whose tiles alone do not fill the chip take two K splits
 extern int g_gn_fa;        // GroupNorm from partials as one fused finalize + apply launch (gn_fa_kernel) at HW <= g_gn_fa
 extern int g_gn_fa_wide;
+extern int g_gn_fa_blocks;
 extern bool g_gn_v2;       // GroupNorm stats v3 (slabbed grid + finalize kernel); 0 = v1 (A/B)
 void group_norm(int dtype, const void* x0, const void* x1, int C0, int C1, int N, int HW, int G, float eps,
                 const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s);
