@@ -251,3 +251,35 @@ def test_vae_fused_groupnorm_slices_bit_exact(device, dtype):
         for k in range(2):
             assert torch.isfinite(res[1][k]).all()
             assert torch.equal(res[1][k], res[0][k]), (n, k)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_unet_reduce_kernel_groupnorm_partials(device, dtype):
+    """The 8x8-level split-K convs' GroupNorm partials from the reduce kernel (splitk_reduce_gn_kernel, option
+    gn_red_parts, default) vs a statistics pass over the stored output (gn_stats3 + gn_finalize3): the same statistics
+    up to fp64 summation order, whose last-bit differences flip 16-bit roundings that the UNet then carries (measured
+    rel L2 5.8e-3 bf16, 1.0e-3 fp16); and each matches its own gn_fa-off form bit for bit (the fold is shared)."""
+    from tests import models_common as MC
+    from image_restoration_and_enhancement_amd.engine import UNet
+    pc, sd = MC.state_dicts("denoise")
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    unet = UNet(pc.unet, dtype, device)
+    unet.load_state_dict(sd["unet"])
+    g = torch.Generator().manual_seed(16)
+    xin = torch.zeros(2, 64, 64, unet.cin_pad)
+    xin[..., :4] = torch.randn(2, 64, 64, 4, generator=g)
+    xin = xin.to(tdt).to(device).contiguous()
+    kv = unet.prepare_context(torch.randn(2, 77, 768, generator=g).to(tdt).to(device).contiguous())
+    t = torch.full((2,), 481.0, device=device)
+    outs = {}
+    for red in (1, 0):
+        for fa in (4096, 0):
+            with L.option(gn_red_parts=red, gn_fa=fa):
+                outs[(red, fa)] = unet.forward(xin, t, kv, 77).float().cpu()
+    for red in (1, 0):
+        assert torch.isfinite(outs[(red, 4096)]).all()
+        assert torch.equal(outs[(red, 4096)], outs[(red, 0)])
+    a, b = outs[(1, 4096)], outs[(0, 4096)]
+    rel = float((a - b).norm() / b.norm())
+    print(f"\nreduce-kernel GroupNorm partials vs stats pass ({dtype}): rel L2 {rel:.2e}")
+    assert rel < (1e-2 if dtype == "bf16" else 2e-3), rel
