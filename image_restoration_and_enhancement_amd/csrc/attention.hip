@@ -1030,7 +1030,8 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
   // query groups per block against resident K/V (cross-attention, Lk <= 2 KT): as many as keep >= 1024 blocks
   const bool res = !CAUSAL && a.Lk <= 2 * KT && g_attn_qrep;
   int qrep = 1;
-  if (res)
+  if (res && g_attn_qrep >= 2) qrep = std::min(g_attn_qrep, 32);   // (sweeps: a forced count)
+  else if (res)
     while (qrep < 8 && ((a.Lq + 128 * 2 * qrep - 1) / (128 * 2 * qrep)) * a.H * a.B >= 1024) qrep *= 2;
   const int nq = (a.Lq + 128 * qrep - 1) / (128 * qrep);
   dim3 grid(nq * a.H * a.B), block(256);
@@ -1144,7 +1145,7 @@ int g_attn_q2 = 1;     // irx_set_option("attn_q2", 0): d = 40 self-attention wi
 int g_attn_pf = 1;     // irx_set_option("attn_pf", 0): d = 40 self-attention without the whole-tile fragment prefetch (A/B)
 int g_attn_xcd = 1;
 int g_attn_prio = 0;
-int g_attn_qrep = 1;   // irx_set_option("attn_qrep", 0): one query group per block in cross-attention (A/B)   // irx_set_option("attn_prio", 1): MFMA chains of attn3 at raised wave priority (A/B)
+int g_attn_qrep = 1;   // irx_set_option("attn_qrep", 0): one query group per block in cross-attention (A/B); >= 2: that many (sweeps)   // irx_set_option("attn_prio", 1): MFMA chains of attn3 at raised wave priority (A/B)
 int g_attn_hm = 1;
 
 }  // namespace irx

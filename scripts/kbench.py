@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--match", default="", help="only shapes whose label contains this")
     ap.add_argument("--ref", action="store_true", help="also time torch (hipBLASLt / MIOpen) on the same shapes")
     ap.add_argument("--variants", default="s2,ring64,small")
+    ap.add_argument("--attn-qrep", action="store_true", help="cross-attention: sweep the resident-K/V query groups")
     args = ap.parse_args()
     dev = torch.device("cuda")
     L.load()
@@ -164,7 +165,11 @@ def main():
             v = torch.randn(B, Lk, C, device=dev, generator=g).to(dt)
             flops = 4.0 * B * Lq * Lk * C
             res = []
-            for vn, opts in (("pf", {"attn_pf": 1, "attn_q2": 0}), ("q2", {"attn_pf": 1, "attn_q2": 1})):
+            avs = (("pf", {"attn_pf": 1, "attn_q2": 0}), ("q2", {"attn_pf": 1, "attn_q2": 1}))
+            if args.attn_qrep and Lk <= 128:   # resident-K/V query groups per block: auto vs forced counts
+                avs = (("auto", {"attn_qrep": 1}),) + tuple((f"qr{q}", {"attn_qrep": q}) for q in (2, 4, 8, 16)) + \
+                      (("auto", {"attn_qrep": 1}),)
+            for vn, opts in avs:
                 with L.option(**opts):
                     ms = timeit(lambda: O.attention(q, k, v, 8), args.iters)
                 res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
