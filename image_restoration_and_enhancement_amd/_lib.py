@@ -119,6 +119,7 @@ _SIGS = {
     "irx_rccl_available": (i32, []),
     "irx_rccl_unique_id": (i32, [C.c_char_p]),
     "irx_rccl_comm_init": (i32, [C.c_char_p, i32, i32, C.POINTER(vp)]),
+    "irx_rccl_comm_init_timeout": (i32, [C.c_char_p, i32, i32, i32, C.POINTER(vp)]),
     "irx_rccl_comm_destroy": (i32, [vp]),
     "irx_rccl_broadcast": (i32, [vp, vp, sz, i32, vp]),
     "irx_weights_bcast": (i32, [vp, vp, i32, vp]),

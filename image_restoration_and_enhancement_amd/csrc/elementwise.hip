@@ -334,15 +334,25 @@ void latent_sample(int dtype, const void* mom, int mcs, int N, int h, int w, con
                                                                     noise, bcast, sf, a, b, out)));
 }
 
+// The 16-bit pack_pixel stores whole 16-byte chunks: the padded width must be a multiple of 8 channels
+// holding the 4 (or 9) live ones, and the destination 16-byte aligned.
+static void check_pack_layout(int dtype, int cin_pad, int inpaint, const void* dst) {
+  if (dtype == F32 || !dst) return;
+  IRX_CHECK(cin_pad % 8 == 0 && cin_pad >= (inpaint ? 16 : 8) && ((uintptr_t)dst % 16) == 0,
+            "16-bit UNet input: cin_pad must be a multiple of 8 (>= 16 for inpaint) and the buffer 16-byte aligned");
+}
+
 void sched_step(const StepArgs& a, hipStream_t s) {
   IRX_CHECK(a.eps && a.x_src && a.x_out, "sched_step: missing buffers");
   IRX_CHECK(!a.inpaint || (a.mask && a.masked && a.cin_pad >= 9), "sched_step: inpaint inputs");
+  check_pack_layout(a.dtype, a.cin_pad, a.inpaint, a.unet_in);
   const long np = (long)a.B * a.h * a.w;
   IRX_DISPATCH(a.dtype, (step_kernel<T><<<nblk(np), kB, 0, s>>>(a)));
 }
 
 void pack_unet_input(int dtype, const float* lat, int B, int h, int w, int cfg, int cin_pad, int inpaint,
                      const float* mask, const float* masked, void* out, hipStream_t s) {
+  check_pack_layout(dtype, cin_pad, inpaint, out);
   const long np = (long)B * h * w;
   IRX_DISPATCH(dtype, (pack_kernel<T><<<nblk(np), kB, 0, s>>>(lat, np, cfg, cin_pad, inpaint, mask, masked,
                                                               (T*)out)));

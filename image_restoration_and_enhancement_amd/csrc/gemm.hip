@@ -307,6 +307,9 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   }
   if (a.dtype != F32 && g_large_tiles && gemm_large_tile(a, s)) return;
   IRX_CHECK(!a.A1, "a two-source A (conv1x1_as_dense) needs the large-tile path");
+  // the 4-wave kernel maps rows through c_off for head-split outputs only: a sub-pixel (up2) output would land at
+  // low-resolution offsets (gemm_up2_ok does not mirror every early exit of gemm_large_tile)
+  IRX_CHECK(!a.up2_w, "a per-parity upsampler conv (up2) needs the large-tile path");
   if (a.dtype == F32) launch_t<float>(a, s);
   else if (a.dtype == F16) launch_t<f16_t>(a, s);
   else launch_t<bf16_t>(a, s);

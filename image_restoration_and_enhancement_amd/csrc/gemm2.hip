@@ -134,8 +134,16 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   const int tiles_n = a.N / BN + (a.N % BN != 0);
   const int tiles_m = (a.M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tile_n = a.nmajor ? bid / tiles_m : bid % tiles_n;
-  const int tile_m = a.nmajor ? bid % tiles_m : bid / tiles_n;
+  int tile_m, tile_n;
+  if (a.group_m > 0) {   // (GemmArgs::group_m) groups of group_m M tiles, N-major inside a group
+    const int gsz = a.group_m * tiles_n, grp = bid / gsz, r = bid - grp * gsz;
+    const int gm = min(a.group_m, tiles_m - grp * a.group_m);
+    tile_m = grp * a.group_m + r % gm;
+    tile_n = r / gm;
+  } else {
+    tile_n = a.nmajor ? bid / tiles_m : bid % tiles_n;
+    tile_m = a.nmajor ? bid % tiles_m : bid / tiles_n;
+  }
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int z = blockIdx.y / sp.splits, ks = blockIdx.y % sp.splits;
   const int nk_all = a.K / BK;
@@ -1662,7 +1670,9 @@ int gemm_emits_gn_parts(const GemmArgs& a) {
   if (c.splits > 1) {   // the in-kernel split-K reduction runs the epilogue; the separate reduce kernel emits them too
     const long tiles = (long)((a.M + c.BM - 1) / c.BM) * ((a.N + c.BN - 1) / c.BN);
     if (!(g_splitk_inkernel && c.splits == 2 && tiles <= kSplitCounters))   // splitk_reduce_gn_kernel
-      return (g_gn_red_parts && !a.up2_w && !c.small && c.BM != 64 && a.M % kRedGnRows == 0 && a.N % 64 == 0 && a.act == ACT_NONE)
+      // (splitk_reduce_gn_kernel applies one bias vector and assumes the plain m * ldc layout: no per-image
+      // weights / bias)
+      return (g_gn_red_parts && !a.up2_w && !a.b_rows && !c.small && c.BM != 64 && a.M % kRedGnRows == 0 && a.N % 64 == 0 && a.act == ACT_NONE)
                  ? kRedGnRows : 0;
   }
   if (a.up2_w && ((long)a.up2_h * a.up2_w) % c.BM) return 0;   // (a sub-pixel tile's rows in one image)
@@ -1745,6 +1755,33 @@ int halo_bn(const GemmArgs& a);
 
 int halo_splits(const GemmArgs& a, long tiles);
 
+// Tile order of a halo conv (GemmArgs::group_m; scheduling only, no numeric effect).  One XCD runs q = tiles / 8
+// consecutive logical tiles at once; in the M-major order they are q / tiles_n M tiles x all tiles_n N tiles, so at
+// the 16x16 level (16 M tiles x 8 N tiles of a 1280-channel conv, 29.5 MB of weights) every XCD streams all of B.
+// Grouped by g M tiles the range is g x q / g: per XCD ~ g halo slabs of A + q / g B panels (bytes (BM + 2W) Cin 2
+// and BN K 2).  g minimises that sum; 0 keeps the M-major order when it is within 10 % of the best.
+int g_halo_group = 1;   // irx_set_option("halo_group", 0): M-major halo tile order (A/B)
+int halo_group_m(const GemmArgs& a, int bn) {
+  if (!g_halo_group) return 0;
+  const long tiles_m = (a.M + 255) / 256, tiles_n = a.N / bn;
+  if (tiles_n < 2) return 0;
+  // logical tiles per XCD (xcd_remap ranges), of which one block per CU = 32 run at a time
+  const long q = (tiles_m * tiles_n + 7) / 8, w = std::min(q, 32L);
+  const double a_m = (256.0 + 2.0 * a.g.Wo) * (a.g.C0 + a.g.C1) * 2.0, b_n = (double)bn * a.K * 2.0;
+  auto cost = [&](long g) {   // A + B bytes of one XCD's w co-resident tiles in groups of g M tiles
+    const bool whole = w >= g * tiles_n;   // (the window spans whole groups: w / tiles_n M tiles x every N tile)
+    const long gm = whole ? (w + tiles_n - 1) / tiles_n : std::min(g, w);
+    const long gn = whole ? tiles_n : (w + g - 1) / g;
+    return gm * a_m + gn * b_n;
+  };
+  const double legacy = cost(std::max(1L, (w + tiles_n - 1) / tiles_n));   // M-major: w / tiles_n whole M rows
+  long best_g = 0;
+  double best = legacy;
+  for (long g = 1; g <= tiles_m; g *= 2)
+    if (cost(g) < best) { best = cost(g); best_g = g; }
+  return best < 0.9 * legacy ? (int)best_g : 0;
+}
+
 size_t gemm_workspace_bytes(const GemmArgs& a) {
   if (!g_large_tiles || !eligible(a)) return 0;
   if (halo_bn(a)) {
@@ -1807,6 +1844,7 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     GemmArgs b = a;
     b.vec_epilogue = 1;
     b.dbg = g_gemm_dbg;
+    b.group_m = halo_group_m(a, hbn);
     Split sp;
     sp.per = a.K / 64;
     const int splits = halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));

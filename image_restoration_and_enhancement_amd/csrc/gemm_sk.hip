@@ -398,6 +398,7 @@ void launch_sk(const GemmArgs& a, hipStream_t s) {
 bool gemm_sk_eligible(const GemmArgs& a) {
   if (!g_gemm_sk || (!a.geglu && g_gemm_sk != 3) || !is16(a.dtype) || a.conv || a.out_f32 || a.batch != 1 || a.K != kSkK) return false;
   if (a.act != ACT_NONE || a.rowadd || a.gn_part || a.gn_ab || a.b_rows || a.ln_out) return false;
+  if (a.A1 || a.up2_w) return false;   // (one A source of K columns; plain row-major output)
   if (a.geglu ? (a.N % 256 != 0 || a.N / 2 / 128 > 32 || a.residual || a.hs_L || a.ldc % 4) : (a.N % 320 || a.N / 320 > 32))
     return false;
   if (a.lda % 8 || a.ldb % 8 || ((uintptr_t)a.A % 16) || ((uintptr_t)a.B % 16)) return false;

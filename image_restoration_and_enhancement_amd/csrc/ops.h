@@ -87,6 +87,10 @@ struct GemmArgs {
   // (set by the launcher) N-major tile order: consecutive tiles (one XCD's range) share a B panel instead of an A
   // panel — for the weight-heavy small-M shapes (8x8-level convs: 29.5 MB of weights for 1024 rows)
   int nmajor = 0;
+  // (set by the launcher, halo convs) grouped tile order: logical tiles run in groups of group_m consecutive M tiles,
+  // N-major inside a group, so one XCD's consecutive range covers a group_m x (range / group_m) rectangle of tiles —
+  // its A slabs and B panels each fetched once into that XCD's L2 (0: the M-major / N-major order above)
+  int group_m = 0;
   int dbg = 0;            // large-tile diagnostics (irx_set_option("gemm_dbg")): 1 skip epilogue, 2 skip MFMAs
 };
 constexpr int kCanonImages = 16;
@@ -168,6 +172,7 @@ extern int g_gn_fuse;      // 1: GroupNorm(+SiLU) folded into the following halo
 extern bool g_large_tiles;
 extern int g_large_mask;
 extern int g_large_dense;
+extern int g_halo_group;   // 1 (default): grouped halo conv tile order where it cuts per-XCD A + B bytes by > 10 %
 extern int g_gemm_nmajor;   // 0 M-major tile order, 1 N-major where B outweighs A (default), 2 always N-major
 extern int g_gemm_deep;    // large-tile pipeline: 0 two-stage BK 64, 1 BK-32 S-stage ring, 2 BK-64 deeper ring
 extern int g_gemm_dbg;     // timing diagnostics only: results are wrong when set

@@ -244,6 +244,12 @@ int irx_median_blur_u8(void* stream, const uint8_t* src, uint8_t* dst, int batch
 int irx_rccl_available(void);                        /* 1 when librccl can be loaded, else 0 */
 int irx_rccl_unique_id(unsigned char* id);           /* id: IRX_RCCL_ID_BYTES bytes (ncclGetUniqueId) */
 int irx_rccl_comm_init(const unsigned char* id, int nranks, int rank, void** comm);   /* ncclCommInitRank */
+/* the same with a deadline: ncclCommInitRankConfig(blocking = 0) polled with ncclCommGetAsyncError; on an error or
+   after timeout_ms the half-made communicator is released with ncclCommAbort, *comm stays NULL and the call fails
+   (irx_last_error says which), so a rank whose peers fail or never arrive leaves the init.  timeout_ms <= 0: the
+   blocking form.  Communicators made this way are non-blocking: irx_rccl_broadcast / irx_weights_bcast wait for
+   each enqueue themselves. */
+int irx_rccl_comm_init_timeout(const unsigned char* id, int nranks, int rank, int timeout_ms, void** comm);
 int irx_rccl_comm_destroy(void* comm);
 int irx_rccl_broadcast(void* comm, void* buf, size_t bytes, int root, void* stream);  /* in place, uint8 */
 /* broadcast the model's bound weight blob (irx_model_bind) from `root`; every rank must have bound a blob of

@@ -83,7 +83,33 @@ E2E_CASES = {
     "cfg4_inpaint_bf16": dict(task="inpaint", res=512, sched="ddim", steps=50, seed=30, batch=8, dtype="bf16"),
     # configs[4]: colorize 768x768, 8 per GPU, 50 DDIM x 0.75 = 37 evals, CFG 7.5, fp16 (src/inference.py:664-672)
     "cfg5_colorize_fp16": dict(task="colorize", res=768, sched="ddim", steps=50, seed=40, batch=8, dtype="fp16"),
+    # The engines that ship (VERDICT r5 "next" #1), on the same inputs and goldens as the case named by `golden`:
+    # the bench engine (bf16 UNet + CLIP, fp16 VAE) at configs[1], and the RestorationPipeline default (all fp16)
+    # at 512x512 denoise (configs[1]) and inpaint (configs[3])
+    "cfg2_denoise_bench": dict(task="denoise", res=512, sched="ddim", steps=50, seed=30, batch=8, dtype="bf16",
+                               vae_dtype="fp16", golden="cfg2_denoise_bf16"),
+    "cfg2_denoise_fp16": dict(task="denoise", res=512, sched="ddim", steps=50, seed=30, batch=8, dtype="fp16",
+                              golden="cfg2_denoise_bf16"),
+    "cfg4_inpaint_fp16": dict(task="inpaint", res=512, sched="ddim", steps=50, seed=30, batch=8, dtype="fp16",
+                              golden="cfg4_inpaint_bf16"),
 }
+
+
+# The reference's own demo fixtures (data/demo/images, data/demo/mask; the inputs app.py:296-330 feeds to
+# `process`), copied into tests/golden/demo/: case -> (task, image file, mask file or None).  Odd sizes give odd
+# latents; the golden of each case is tests/golden/demo_<case>.npz (tests/golden/make_golden_demo.py).
+DEMO_CASES = {
+    "denoise1": ("denoise", "denoise1.jpg", None),                          # 500x333 RGB  -> 496x328, 62x41
+    "denoise2": ("denoise", "denoise2.jpg", None),                          # 640x457 RGB  -> 640x456, 80x57
+    "sr0": ("sr", "super-resolution.jpg", None),                            # 160x114 RGB  -> 160x112, 20x14
+    "sr1": ("sr", "super-resolution1.jpg", None),                           # 125x83 RGB   -> 120x80, 15x10
+    "colorize1": ("colorize", "colorize1.png", None),                       # 500x333 L    -> 62x41
+    "colorize2": ("colorize", "colorize2.png", None),                       # 640x457 L    -> 80x57
+    "inpaint1": ("inpaint", "inpaint1.jpg", "000000006471_mask.jpg"),       # 500x333 -> 512x512, 64x64
+    "inpaint2": ("inpaint", "inpaint2.jpg", "000000020247_mask.jpg"),       # 640x457 -> 512x512, 64x64
+}
+DEMO_LATENTS = {"denoise1": "62x41", "denoise2": "80x57", "sr0": "20x14", "sr1": "15x10", "colorize1": "62x41",
+                "colorize2": "80x57", "inpaint1": "64x64", "inpaint2": "64x64"}
 
 
 def weight_fingerprint(sd: dict) -> np.ndarray:

@@ -2,6 +2,7 @@
 contiguous batch sharding, the frozen-weight blob broadcast, the end-of-job output gather and the
 max-over-ranks timing reduction bench.py uses.  The same code runs over RCCL ("nccl") on MI355X."""
 import os
+import time
 import socket
 
 import pytest
@@ -72,6 +73,9 @@ def test_gloo_world2_broadcast_gather_max():
         assert mx == 2.5
 
 
+INIT_TIMEOUT_S = 2.0
+
+
 class _Model:
     """Stand-in for a bound irx model: a handle and its packed weight blob."""
 
@@ -82,8 +86,9 @@ class _Model:
 def _stub_lib(L, rank, scenario, models, log):
     """_lib.call replaced by a stub: the RCCL entry points succeed or fail per `scenario`, and irx_weights_bcast
     moves the blob with a gloo broadcast so the data path can be checked end to end on the CPU.  The stubbed
-    irx_rccl_comm_init returns at once on every rank: it does not model RCCL's blocking (collective) init, where a
-    rank failing partway can leave its peers waiting inside ncclCommInitRank (dist.rccl_comm docstring)."""
+    irx_rccl_comm_init_timeout models the C side's deadline: in scenario "inithang" rank 1's init never completes
+    and rank 0's waits for it (the init is collective), so both return the C ABI's timeout error once
+    `timeout_ms` has passed (the real form aborts the half-made communicator there: tests/test_rccl_gpu.py)."""
     import ctypes as C
     import torch.distributed as dist
     uid = bytes(range(128))
@@ -97,11 +102,15 @@ def _stub_lib(L, rank, scenario, models, log):
                 raise L.IrxError("ncclGetUniqueId: stub failure")
             C.memmove(args[0], uid, len(uid))
             return 0
-        if name == "irx_rccl_comm_init":
-            idb, world, r, pcomm = args
-            assert bytes(idb)[:128] == uid and world == 2 and r == rank
+        if name == "irx_rccl_comm_init_timeout":
+            idb, world, r, timeout_ms, pcomm = args
+            assert bytes(idb)[:128] == uid and world == 2 and r == rank and timeout_ms >= 1
             if scenario == "initfail" and rank == 1:
-                raise L.IrxError("ncclCommInitRank: stub failure")
+                raise L.IrxError("ncclCommInitRankConfig: stub failure")
+            if scenario == "inithang":
+                time.sleep(timeout_ms / 1000.0)
+                raise L.IrxError(f"ncclCommInitRankConfig: rank {rank} of 2 did not finish within {timeout_ms} ms "
+                                 "(communicator aborted)")
             pcomm._obj.value = 1000 + rank
             return 0
         if name == "irx_rccl_comm_destroy":
@@ -118,7 +127,7 @@ def _stub_lib(L, rank, scenario, models, log):
 
 def _bcast_worker(rank, world, port, scenario, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), IRX_RCCL_INIT_TIMEOUT_S=str(INIT_TIMEOUT_S))
     try:
         from image_restoration_and_enhancement_amd import _lib as L
         D.init("gloo")
@@ -128,23 +137,27 @@ def _bcast_worker(rank, world, port, scenario, q):
         models = {k: _Model(i + 1, v.clone() if rank == 0 else torch.zeros_like(v)) for i, (k, v) in enumerate(ref.items())}
         log = []
         L.call = _stub_lib(L, rank, scenario, models, log)
+        D.barrier()
+        t0 = time.monotonic()
         how = D.broadcast_models(models)
+        dt = time.monotonic() - t0
         ok = all(torch.equal(models[k].blob, ref[k]) for k in ref)
         D.barrier()
-        q.put((rank, how.split(" ")[0], ok, log.count("irx_rccl_comm_destroy"), log.count("irx_weights_bcast")))
+        q.put((rank, how.split(" ")[0], ok, log.count("irx_rccl_comm_destroy"), log.count("irx_weights_bcast"), dt))
     except Exception as ex:  # report instead of hanging the parent
-        q.put((rank, repr(ex), None, None, None))
+        q.put((rank, repr(ex), None, None, None, None))
     finally:
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("scenario", ["ok", "nolib", "noid", "initfail"])
+@pytest.mark.parametrize("scenario", ["ok", "nolib", "noid", "initfail", "inithang"])
 def test_broadcast_models_rank_consistent(scenario):
-    """dist.broadcast_models with _lib.call stubbed: every rank takes the same path —
-    irx_weights_bcast when RCCL comes up everywhere, the torch.distributed broadcast on every rank when librccl is
-    missing on one rank, rank 0 cannot make the unique id, or one rank's communicator init fails (the ranks that got
-    a communicator destroy it) — and the blobs arrive intact either way."""
+    """dist.broadcast_models with _lib.call stubbed: every rank takes
+    the same path — irx_weights_bcast when RCCL comes up everywhere, the torch.distributed broadcast on every rank
+    when librccl is missing on one rank, rank 0 cannot make the unique id, one rank's communicator init fails (the
+    ranks that got a communicator destroy it), or one rank's init hangs (every rank leaves within the deadline) —
+    and the blobs arrive intact either way."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -155,8 +168,10 @@ def test_broadcast_models_rank_consistent(scenario):
     for p in procs:
         p.join(timeout=60)
     want = "irx_rccl" if scenario == "ok" else "torch.distributed"
-    for rank, how, ok, destroyed, bcasts in res:
+    for rank, how, ok, destroyed, bcasts, dt in res:
         assert how == want, (rank, how)
+        if scenario == "inithang":   # out within the deadline (+ the agreement round trips and the fallback)
+            assert INIT_TIMEOUT_S <= dt < INIT_TIMEOUT_S + 20, (rank, dt)
         assert ok is True
         assert bcasts == (2 if scenario == "ok" else 0)
         exp_destroy = 1 if scenario == "ok" or (scenario == "initfail" and rank == 0) else 0

@@ -42,6 +42,15 @@ GOLDEN = Path(__file__).resolve().parent / "golden"
 PSNR_MIN = {"cfg2_denoise_bf16": 45.0, "cfg3_sr_bf16": 47.0, "cfg4_inpaint_bf16": 45.5, "cfg5_colorize_fp16": 55.0}
 REL_MAX = {"cfg2_denoise_bf16": 1.25e-2, "cfg3_sr_bf16": 9.5e-3, "cfg4_inpaint_bf16": 1.15e-2, "cfg5_colorize_fp16": 5e-3}
 LAT_MAX = {"cfg2_denoise_bf16": 9.5e-3, "cfg3_sr_bf16": 3e-3, "cfg4_inpaint_bf16": 1e-2, "cfg5_colorize_fp16": 1.8e-3}
+# The shipped engines on the cfg2 / cfg4 goldens (VERDICT r5 "next" #1): bench engine = bf16 UNet + CLIP with an
+# fp16 VAE; fp16 = the RestorationPipeline default.  Measured round 6 (profiles/r06_gpu_tests_parity.txt, rows 0 / last):
+#   cfg2_denoise_bench   54.76 / 54.79 dB   rel L2 3.40e-3   latents 4.67e-3   (u8 max 2)
+#   cfg2_denoise_fp16    59.90 / 59.92 dB   rel L2 2.51e-3   latents 6.33e-4   (u8 max 1)
+#   cfg4_inpaint_fp16    60.36 / 60.40 dB   rel L2 2.45e-3   latents 5.94e-4   (u8 max 1)
+# same rule: 5 dB under the measured PSNR, 2x the measured relative errors
+PSNR_MIN.update({"cfg2_denoise_bench": 49.5, "cfg2_denoise_fp16": 54.5, "cfg4_inpaint_fp16": 55.0})
+REL_MAX.update({"cfg2_denoise_bench": 7e-3, "cfg2_denoise_fp16": 5e-3, "cfg4_inpaint_fp16": 5e-3})
+LAT_MAX.update({"cfg2_denoise_bench": 9.5e-3, "cfg2_denoise_fp16": 1.3e-3, "cfg4_inpaint_fp16": 1.2e-3})
 
 
 def _golden(name):
@@ -55,11 +64,13 @@ def run_case(device, name):
     c = MC.E2E_CASES[name]
     task = c["task"]
     model_task = "inpaint" if task == "inpaint" else "denoise"
-    g = _golden(name)
+    gname = c.get("golden", name)
+    g = _golden(gname)
     pc, sd = MC.state_dicts(model_task)
     for k in ("unet", "vae", "clip"):
         assert np.array_equal(MC.weight_fingerprint(sd[k]), g[f"fp_{k}"]), f"{k} weights differ from the golden's"
-    eng = SDEngine(PipelineConfig.default(model_task), c["dtype"], device, state_dicts=sd)
+    eng = SDEngine(PipelineConfig.default(model_task), c["dtype"], device, state_dicts=sd,
+                   vae_dtype=c.get("vae_dtype"))
     eng.cfg.scheduler.kind = c["sched"]
     prompt, strength, _, guidance = PR.TASKS[task]
     imgs, masks = MC.task_images(task, c["res"], c["batch"], c["seed"])
@@ -93,7 +104,7 @@ def run_case(device, name):
     ms = [metrics(0, g)]
     if c["batch"] > 1:
         # the batch's last row: its rows sit at the end of the batch, away from the row-tile starts
-        gl = _golden(f"{name}_last")
+        gl = _golden(f"{gname}_last")
         assert int(gl["row"]) == c["batch"] - 1 and gl["timesteps"].tolist() == got.timesteps
         ms.append(metrics(c["batch"] - 1, gl))
     for m in ms:
@@ -108,10 +119,12 @@ def test_e2e_cfg1_fp32_full_pndm(device):
     assert m["max_abs"] < 1e-3 and m["u8_max"] <= 1 and m["lat_rel_max"] < 1e-4, m
 
 
-@pytest.mark.parametrize("name", ["cfg2_denoise_bf16", "cfg3_sr_bf16", "cfg4_inpaint_bf16", "cfg5_colorize_fp16"])
+@pytest.mark.parametrize("name", ["cfg2_denoise_bf16", "cfg3_sr_bf16", "cfg4_inpaint_bf16", "cfg5_colorize_fp16",
+                                  "cfg2_denoise_bench", "cfg2_denoise_fp16", "cfg4_inpaint_fp16"])
 def test_e2e_16bit_full_length(device, name):
     ms = run_case(device, name)
-    want = {"cfg2_denoise_bf16": 25, "cfg3_sr_bf16": 40, "cfg4_inpaint_bf16": 30, "cfg5_colorize_fp16": 37}[name]
+    want = {"cfg2_denoise_bf16": 25, "cfg3_sr_bf16": 40, "cfg4_inpaint_bf16": 30, "cfg5_colorize_fp16": 37,
+            "cfg2_denoise_bench": 25, "cfg2_denoise_fp16": 25, "cfg4_inpaint_fp16": 30}[name]
     assert len(ms) == 2                 # row 0 and the last row, same bars
     for m in ms:
         assert m["evals"] == want
