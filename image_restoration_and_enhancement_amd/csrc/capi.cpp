@@ -93,6 +93,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"arena_guard", &g_arena_guard, nullptr},
     {"gemm_nmajor", &g_gemm_nmajor, nullptr},
     {"halo_group", &g_halo_group, nullptr},
+    {"halo_strip", &g_halo_strip, nullptr},
     {"prof_shapes", &g_prof_shapes, nullptr},
     {"attn_prio", &g_attn_prio, nullptr},
     {"attn_qrep", &g_attn_qrep, nullptr},

@@ -106,6 +106,10 @@ __device__ __forceinline__ void glds16_s(uint32_t voff, const void* base, uint32
 // one halo + 9 B panels instead of 9 A panels + 9 B panels (1.5x fewer L2 -> LDS bytes per MFMA at
 // 256x160 than the 256x320 im2col tile), with whole 128-B lines per request (BK 64).
 constexpr int kHaloWMax = 64;    // widest image row a halo tile takes (LDS: 2 x (BM + 2W) x 2BK B)
+// strip halo tiles (HALO == 5): 8 rows x 32 columns; halo 10 x 32 pixels + the neighbouring columns at halo pixels
+// kStripEdgeL + h / kStripEdgeR + h (h = halo row 0..9), inside the (BM + 2 kHaloWMax)-pixel halo buffer
+constexpr int kStripW = 32, kStripEdgeL = 320, kStripEdgeR = 336;
+static_assert(kStripEdgeR + 16 <= 256 + 2 * kHaloWMax, "strip halo edge columns");
 
 template <typename T, int BM, int BN, int WM, int WN, int BK, int S, bool CONV, bool OUTF32, bool RESIZE,
           int HALO = 0, bool PP = false>
@@ -121,6 +125,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   constexpr int KSUB = BK / 32;              // 32-deep MFMA sub-steps per stage
   static_assert((NW == 8 || NW == 4) && ROWS % RPI == 0 && BM % 16 == 0 && (BK == 32 || BK == 64), "tile shape");
   static_assert(!HALO || (CONV && !RESIZE && S >= 2 && S <= 8 && NW == 8), "halo tiles: 3x3 conv");
+  // HALO == 5: the ping-pong halo loop over 8-row x 32-column strip tiles (images wider than kHaloWMax, or rows
+  // that are no power of two): the tile's GEMM rows are the strip's pixels in (row, column) order (host: the
+  // tiles of an image are its strips, row block major), the halo is 10 rows x 32 columns plus the two
+  // neighbouring columns (kept in the halo buffer's spare pixel rows), and the epilogue maps rows to NHWC pixels
+  constexpr bool STRIP = HALO == 5;
   constexpr int HB_U4 = (BM + 2 * kHaloWMax) * CPR;   // one halo slab buffer (uint4)
   constexpr int RING = HALO ? 2 * HB_U4 + S * BN * CPR + CPR + 64 : S * STAGE;
   // (+ a scratch KiB for the surplus DMA pieces, inside the epilogue's staging area when the ring is smaller)
@@ -293,7 +302,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     }
   };
 
-  if constexpr (HALO == 2 || HALO == 4) {
+  if constexpr (HALO == 2 || HALO == 4 || HALO == 5) {
     // ---- ping-pong halo main loop (the default halo path; no GroupNorm-fused operand).  The two waves that
     //      share a SIMD (w and w + 4) take opposite roles in each half of a K step (slab c = kt / 9, tap
     //      t = kt % 9), so one of them always has MFMAs to issue while the other moves data:
@@ -318,9 +327,18 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     static_assert(S == 3 && KSUB == 2 && NW == 8 && CPR == 8 && RPI == 8, "ping-pong halo: 3-stage B ring, BK 64");
     constexpr bool DG = HALO == 4;
     const int dbg = DG ? a.dbg : 0;
-    const int W = a.g.Win, H = a.g.Hin, lw = __builtin_ctz(W);
+    const int W = a.g.Win, H = a.g.Hin;
+    const int Wl = STRIP ? kStripW : W, lw = __builtin_ctz(Wl);   // pixels per halo row in LDS
     const int HW = H * W;
-    const int img = m0 / HW, y0 = (m0 - img * HW) >> lw;
+    const int img = m0 / HW;
+    int y0, x0 = 0;   // the tile's first output row / column
+    if constexpr (STRIP) {
+      const int t = (m0 - img * HW) / BM, ns = W / kStripW, rb = t / ns;
+      y0 = rb * (BM / kStripW);
+      x0 = (t - rb * ns) * kStripW;
+    } else {
+      y0 = (m0 - img * HW) >> lw;
+    }
     const int nhi = (((BM >> lw) + 2) << lw) / RPI;   // halo wave-instructions (RPI pixel rows each)
     constexpr int NG = NW / 2;                        // waves per group
     constexpr int HPG = (BM + 2 * kHaloWMax) / RPI / NG;   // halo pieces per group-0 wave per slab
@@ -343,13 +361,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     // ---- halo rows outside the image (top / bottom tiles): zero in both buffers once, never DMA'd
     {
       const int ylo = y0 - 1, yhi = y0 + (BM >> lw);   // the halo's first / last image row
-      for (int i = tid; i < 2 * (W * CPR); i += NT) {
-        const int side = i / (W * CPR), k = i - side * (W * CPR);
+      for (int i = tid; i < 2 * (Wl * CPR); i += NT) {
+        const int side = i / (Wl * CPR), k = i - side * (Wl * CPR);
         const bool out = side == 0 ? ylo < 0 : yhi >= H;
         const int hrow = side == 0 ? 0 : (BM >> lw) + 1;
         if (out) {
-          Hb[hrow * W * CPR + k] = uint4{0u, 0u, 0u, 0u};
-          Hb[HB_U4 + hrow * W * CPR + k] = uint4{0u, 0u, 0u, 0u};
+          Hb[hrow * Wl * CPR + k] = uint4{0u, 0u, 0u, 0u};
+          Hb[HB_U4 + hrow * Wl * CPR + k] = uint4{0u, 0u, 0u, 0u};
         }
       }
     }
@@ -366,9 +384,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
       for (int j = 0; j < BPG; ++j) glds16_s(voffB, b + j * pstrB, m + j * 1024u);
     };
-    // group 0: halo piece q = gw * HPG + j of slab c = pixels RPI * q .. + 7 of the (rows + 2) x W halo, which
-    // starts at image pixel P0 = (img * H + y0 - 1) * W; a piece is wholly inside or outside the image
-    const long P0 = (long)(img * H + y0 - 1) * W;
+    // group 0: halo piece q = gw * HPG + j of slab c = pixels RPI * q .. + 7 of the (rows + 2) x Wl halo, which
+    // starts at image pixel P0 = (img * H + y0 - 1) * W + x0; a piece is wholly inside or outside the image.
+    // STRIP: a halo row is 32 pixels (4 pieces); pieces nhi .. nhi + 3 are the neighbouring columns x0 - 1 (halo
+    // rows 0-7, 8-9) and x0 + 32 (same), at halo pixels 320 + h / 336 + h, their lanes each on their own pixel
+    // (zeros for pixels outside the image)
+    const long P0 = (long)(img * H + y0 - 1) * W + x0;
     const long Plo = (long)img * HW, Phi = Plo + HW;
     const uint32_t voffH0 = (uint32_t)(lr * a.g.C0 + lch * 8) * 2u;
     const uint32_t voffH1 = (uint32_t)(lr * a.g.C1 + lch * 8) * 2u;
@@ -383,9 +404,25 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
       for (int j = j0; j < j1; ++j) {
         const int q = gw * HPG + j;
-        const long P = P0 + RPI * q;
-        const bool ok = q < nhi && P >= Plo && P < Phi;
-        glds16_s(vo, ok ? sb + (P * cs + ch) * 2 : sb, ok ? mb + (uint32_t)q * 1024u : ldsX);
+        if constexpr (STRIP) {
+          if (q >= nhi && q < nhi + 4) {   // a neighbouring column: per-lane addresses (one pixel per lane row)
+            const int e = q - nhi, hr = (e & 1) * RPI + lr, yy = y0 - 1 + hr;
+            const int col = (e >> 1) ? x0 + kStripW : x0 - 1;
+            const bool v = hr < (BM >> lw) + 2 && (unsigned)yy < (unsigned)H && (unsigned)col < (unsigned)W;
+            const uint16_t* src =
+                v ? (const uint16_t*)sb + ((long)(img * H + yy) * W + col) * cs + ch + lch * 8 : zp;
+            glds16_asm(src, mb + (uint32_t)q * 1024u);
+            continue;
+          }
+          const int hr = q >> 2;   // (kStripW / RPI = 4 pieces per halo row)
+          const long P = P0 + (long)hr * W + (q & 3) * RPI;
+          const bool ok = q < nhi && (unsigned)(y0 - 1 + hr) < (unsigned)H;
+          glds16_s(vo, ok ? sb + (P * cs + ch) * 2 : sb, ok ? mb + (uint32_t)q * 1024u : ldsX);
+        } else {
+          const long P = P0 + RPI * q;
+          const bool ok = q < nhi && P >= Plo && P < Phi;
+          glds16_s(vo, ok ? sb + (P * cs + ch) * 2 : sb, ok ? mb + (uint32_t)q * 1024u : ldsX);
+        }
       }
     };
     // ---- fragment addressing, hoisted out of the K loop.  With the 9 taps of a slab unrolled, the tap (ky, kx)
@@ -401,14 +438,19 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       for (int kx = 0; kx < 3; ++kx) aoff[kx][ss] = frow * CPR + (ck ^ ((frow + kx - 1) & 7));
       boff[ss] = frow * CPR + (ck ^ (frow & 7));
     }
-    const int awave = wm * TM * 16 * CPR, bwave = wn * TN * 16 * CPR, rowW = W * CPR;
+    const int awave = wm * TM * 16 * CPR, bwave = wn * TN * 16 * CPR, rowW = Wl * CPR;
     bool zl[TM], zr[TM];   // fragment rows at the image's left / right edge: taps kx = 0 / 2 read the zero row
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int rx = (wm * TM * 16 + i * 16 + frow) & (W - 1);
+      const int rx = (wm * TM * 16 + i * 16 + frow) & (Wl - 1);
       zl[i] = rx == 0;
-      zr[i] = rx == W - 1;
+      zr[i] = rx == Wl - 1;
     }
+    // STRIP: the strip row of fragment i (its 16 rows lie in one 32-pixel strip row: wave-uniform); its edge lanes
+    // read the neighbouring column's pixel of halo row eh + ky, logical chunk ck at slot ck ^ ((eh + ky) & 7)
+    int eh[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) eh[i] = __builtin_amdgcn_readfirstlane((wm * TM * 16 + i * 16) >> lw);
     uint4 fa[KSUB][TM], fb[KSUB][TN];
     auto readF = [&](auto tc, const uint4* Hs) {   // this wave's fragments of tap t (both 32-deep sub-steps)
       constexpr int t = decltype(tc)::value, ky = t / 3, kx = t % 3, st = t % S;
@@ -420,8 +462,16 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const uint4* src = Hrow + aoff[kx][ss] + i * 16 * CPR;
-          if constexpr (kx == 0) src = zl[i] ? zrow + ss * 4 + fgrp : src;
-          if constexpr (kx == 2) src = zr[i] ? zrow + ss * 4 + fgrp : src;
+          if constexpr (STRIP) {
+            if constexpr (kx != 1) {
+              const int h = eh[i] + ky;
+              const uint4* e = Hs + ((kx == 0 ? kStripEdgeL : kStripEdgeR) + h) * CPR + ((ss * 4 + fgrp) ^ (h & 7));
+              src = (kx == 0 ? zl[i] : zr[i]) ? e : src;
+            }
+          } else {
+            if constexpr (kx == 0) src = zl[i] ? zrow + ss * 4 + fgrp : src;
+            if constexpr (kx == 2) src = zr[i] ? zrow + ss * 4 + fgrp : src;
+          }
           fa[ss][i] = *src;
         }
 #pragma unroll
@@ -954,6 +1004,18 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 
   // ---- epilogue (D[row = 4g + r][col = lane & 15] per 16x16 tile)
   const uint16_t* __restrict__ Rp = a.residual ? (const uint16_t*)a.residual + (long)z * a.sR : nullptr;
+  // NHWC pixel row of GEMM row m (STRIP: the tiles of an image are its 8 x 32 strips, row block major, and a tile's
+  // rows its pixels in (row, column) order; the row add and GroupNorm partials index images / tiles, unchanged)
+  auto prow = [&](long m) -> long {
+    if constexpr (STRIP) {
+      const int HW = a.g.Hin * a.g.Win, W = a.g.Win;
+      const long im = m / HW;
+      const int t = (int)(m - im * HW), blk = t / BM, r = t - blk * BM, ns = W / kStripW, rb = blk / ns;
+      return im * HW + (long)(rb * (BM / kStripW) + r / kStripW) * W + (blk - rb * ns) * kStripW + r % kStripW;
+    } else {
+      return m;
+    }
+  };
   if constexpr (!OUTF32) {
     if (a.vec_epilogue) {
       // Staged through LDS: pass 1 (every wave) applies alpha/bias/row-add/act and writes the bf16 tile
@@ -1037,7 +1099,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       auto fetch = [&](int row, int c, Src& q) {
         const int m = m0 + row, n = n0 + c * 8;
         q.u = *(const uint4*)(tileS + row * BN + (csw(c, row) << 3));
-        if (Rp) q.r = *(const uint4*)(Rp + (long)m * a.ldr + n);
+        if (Rp) q.r = *(const uint4*)(Rp + prow(m) * a.ldr + n);
         if (a.rowadd) {
           const float4* ra = (const float4*)(a.rowadd + (long)(m / a.rows_per_group) * a.rowadd_ld + n);
           q.x = ra[0];
@@ -1064,7 +1126,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           for (int e = 0; e < 8; ++e) f[e] *= a.out_scale;
           u = Vec16<T>::pack(f);
         }
-        *(uint4*)(Cp + c_off(a, m, n)) = u;
+        *(uint4*)(Cp + c_off(a, prow(m), n)) = u;
         return u;
       };
       if (a.gn_part && NT >= BN) {
@@ -1118,7 +1180,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
                 for (int u = 0; u < kEpiPF; ++u) {
                   const int row = min(rg + (k0 + u) * RS, rend - 1);
-                  rres[u] = *(const uint4*)(Rp + (long)(m0 + row) * a.ldr + n0 + cc * 8);
+                  rres[u] = *(const uint4*)(Rp + prow(m0 + row) * a.ldr + n0 + cc * 8);
                 }
               }
 #pragma unroll
@@ -1240,7 +1302,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           }
           if (Rp) {
             float rv[8];
-            Vec16<T>::unpack(*(const uint4*)(Rp + (long)m * a.ldr + n), rv);
+            Vec16<T>::unpack(*(const uint4*)(Rp + prow(m) * a.ldr + n), rv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] += rv[e];
           }
@@ -1249,7 +1311,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           u = Vec16<T>::pack(f);
           if (lno) *ts = u;
         }
-        *(uint4*)(Cp + c_off(a, m, n)) = u;
+        *(uint4*)(Cp + c_off(a, prow(m), n)) = u;
       };
       // (one chunk per step: batching the residual loads of 8 steps measured no faster, 31.9 vs 31.9 us at the
       //  64^2-level to_out shape, profiles/r05_kbench_gemm_res.txt)
@@ -1637,8 +1699,10 @@ int g_gemm_force = 0;            // irx_set_option("gemm_force", BM*100000 + BN*
 int g_gn_fuse = 0;   // measured slower: the halo normalisation's VALU work does not hide under the MFMAs
 int halo_bn(const GemmArgs& a);
 
-bool gemm_gn_fusable(const GemmArgs& a) {
-  return g_gn_fuse && g_large_tiles && is16(a.dtype) && eligible(a) && halo_bn(a) != 0;
+int halo_mode(const GemmArgs& a);
+
+bool gemm_gn_fusable(const GemmArgs& a) {   // (the lock-step halo loop, HALO == 1: 160-wide row tiles only)
+  return g_gn_fuse && g_large_tiles && is16(a.dtype) && eligible(a) && halo_bn(a) == 160 && halo_mode(a) == 1;
 }
 
 int g_conv1x1_dense = 1;   // irx_set_option("conv1x1_dense", 0): 1x1 convs on the im2col conv path (A/B)
@@ -1767,7 +1831,8 @@ int halo_group_m(const GemmArgs& a, int bn) {
   if (tiles_n < 2) return 0;
   // logical tiles per XCD (xcd_remap ranges), of which one block per CU = 32 run at a time
   const long q = (tiles_m * tiles_n + 7) / 8, w = std::min(q, 32L);
-  const double a_m = (256.0 + 2.0 * a.g.Wo) * (a.g.C0 + a.g.C1) * 2.0, b_n = (double)bn * a.K * 2.0;
+  const double hpix = halo_mode(a) == 2 ? 10.0 * (kStripW + 2) : 256.0 + 2.0 * a.g.Wo;   // halo pixels per tile
+  const double a_m = hpix * (a.g.C0 + a.g.C1) * 2.0, b_n = (double)bn * a.K * 2.0;
   auto cost = [&](long g) {   // A + B bytes of one XCD's w co-resident tiles in groups of g M tiles
     const bool whole = w >= g * tiles_n;   // (the window spans whole groups: w / tiles_n M tiles x every N tile)
     const long gm = whole ? (w + tiles_n - 1) / tiles_n : std::min(g, w);
@@ -1784,8 +1849,8 @@ int halo_group_m(const GemmArgs& a, int bn) {
 
 size_t gemm_workspace_bytes(const GemmArgs& a) {
   if (!g_large_tiles || !eligible(a)) return 0;
-  if (halo_bn(a)) {
-    const int sp = halo_splits(a, canon_rows(a) / 256 * (a.N / 160));
+  if (const int hbn = halo_bn(a)) {
+    const int sp = halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));
     return sp > 1 ? (size_t)sp * a.M * a.N * sizeof(float) : 0;
   }
   const Choice c = choose(a);
@@ -1813,18 +1878,34 @@ int halo_splits(const GemmArgs& a, long tiles) {
   return 0;
 }
 
-// Halo tile (BN) for a 3x3 / stride-1 / pad-1 conv whose 256-pixel tiles are whole image rows and whose
-// grid fills the chip (alone or with two K splits); 0 = not applicable.
-int halo_bn(const GemmArgs& a) {
+// irx_set_option("halo_strip", m): 0 no strip tiles (VAE / 768^2 convs on the im2col walk, A/B), 1 (default) strip
+// tiles where whole-row tiles do not fit (W > 64 or no power of two), 2 strip tiles wherever the shape allows (tests:
+// strips == rows bit for bit at W <= 64)
+int g_halo_strip = 1;
+
+// Halo tile mode of a 3x3 / stride-1 / pad-1 conv: 1 = 256-pixel tiles of whole image rows (W in {16, 32, 64}),
+// 2 = 8 x 32 strip tiles (W % 32 == 0, H % 8 == 0; HALO == 5), 0 = neither
+int halo_mode(const GemmArgs& a) {
   const ConvGeom& g = a.g;
   if (!g_conv_halo || !a.conv || a.batch != 1 || a.geglu || a.out_f32 || !vec_ok(a)) return 0;
   if (g.KH != 3 || g.KW != 3 || g.stride != 1 || g.pad_t != 1 || g.pad_l != 1) return 0;
   if (g.Hv != g.Hin || g.Wv != g.Win || g.Ho != g.Hin || g.Wo != g.Win) return 0;
   if (g.C0 % 64 || g.C1 % 64 || g.C0 <= 0) return 0;
   const int W = g.Win;
-  if (W < 16 || W > kHaloWMax || (W & (W - 1)) || 256 % W || g.Hin % (256 / W)) return 0;
   if ((long)g.N * g.Hin * W != a.M || a.M % 256) return 0;
-  const int bn = a.N % 160 == 0 ? 160 : 0;
+  const bool rows = W >= 16 && W <= kHaloWMax && !(W & (W - 1)) && 256 % W == 0 && g.Hin % (256 / W) == 0;
+  // (strips: the ping-pong loop only, no GroupNorm-fused operand)
+  const bool strips = g_halo_strip && g_halo_pipe && !a.gn_ab && W % kStripW == 0 && g.Hin % (256 / kStripW) == 0;
+  if (strips && (g_halo_strip == 2 || !rows)) return 2;
+  return rows ? 1 : 0;
+}
+
+// Halo tile (BN) for a 3x3 / stride-1 / pad-1 conv on halo tiles (halo_mode) whose grid fills the chip (alone or with
+// two K splits); 0 = not applicable.  BN 160 (UNet widths), else 128 (VAE widths 128 / 256 / 512; ping-pong loop only)
+int halo_bn(const GemmArgs& a) {
+  const int mode = halo_mode(a);
+  if (!mode) return 0;
+  const int bn = a.N % 160 == 0 ? 160 : (a.N % 128 == 0 && g_halo_pipe && !a.gn_ab) ? 128 : 0;
   if (!bn || !halo_splits(a, canon_rows(a) / 256 * (a.N / bn))) return 0;
   // (GroupNorm-fused operand: one 512-element chunk of the (256 + 2W) x 8 halo per tap, taps 3..8)
   static_assert((256 + 2 * kHaloWMax) * 8 <= 512 * 6, "halo normalisation chunks");
@@ -1863,8 +1944,15 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     if (g_halo_pipe && !a.gn_ab && b.dbg && a.dtype == BF16) launch2<256, 160, 4, 2, 64, 3, 4>(b, sp, s);   // (diagnostics)
     else
 #endif
-    if (g_halo_pipe && !a.gn_ab) launch2<256, 160, 4, 2, 64, 3, 2>(b, sp, s);   // ping-pong main loop
-    else launch2<256, 160, 4, 2, 64, 3, 1>(b, sp, s);
+    if (halo_mode(a) == 2) {            // strip tiles (ping-pong main loop)
+      if (hbn == 160) launch2<256, 160, 4, 2, 64, 3, 5>(b, sp, s);
+      else launch2<256, 128, 4, 2, 64, 3, 5>(b, sp, s);
+    } else if (g_halo_pipe && !a.gn_ab) {   // ping-pong main loop
+      if (hbn == 160) launch2<256, 160, 4, 2, 64, 3, 2>(b, sp, s);
+      else launch2<256, 128, 4, 2, 64, 3, 2>(b, sp, s);
+    } else {
+      launch2<256, 160, 4, 2, 64, 3, 1>(b, sp, s);
+    }
     return true;
   }
   const Choice c = choose(a);

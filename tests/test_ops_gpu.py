@@ -758,3 +758,76 @@ def test_conv1x1_two_source_dense(device, dt, N, H, W, C0, C1, Co, res):
     assert torch.isfinite(outs[0].float()).all()
     assert O.rel_err(outs[0], ref) < TOL[dt]
     assert O.rel_err(outs[0], outs[1].float()) < 2e-3
+
+
+# ------------------------------------------------------------------ strip halo tiles (8 rows x 32 columns)
+@pytest.mark.parametrize("case", [
+    # (N, H, W, C0, C1, Cout, rowadd+residual): the VAE's widths (BN 128) at W > 64, the 768^2 UNet's 96-wide
+    # level (BN 160), a concat, ragged strip counts (W 96 / 160), BN 128 on whole-row tiles (W 64)
+    (1, 16, 128, 128, 0, 128, True),
+    (2, 8, 256, 256, 0, 256, False),
+    (1, 8, 512, 128, 0, 128, True),
+    (1, 16, 96, 320, 0, 320, True),
+    (1, 8, 160, 64, 64, 128, True),
+    (1, 24, 64, 512, 0, 512, True),
+])
+@pytest.mark.parametrize("dt", DT16)
+def test_conv_halo_strip(device, halo_forced, case, dt):
+    """Strip halo tiles (HALO == 5, option halo_strip) and the 128-wide halo tiles vs the fp32 CPU conv: the
+    neighbouring columns of every strip, the image's left / right / top / bottom zero padding, the epilogue's
+    row -> NHWC pixel mapping for the store, the residual and the row add."""
+    N, H, W, C0, C1, Co, extra = case
+    x0 = _r(N, C0, H, W, seed=380)
+    x1 = _r(N, C1, H, W, seed=381) if C1 else None
+    w = _r(Co, C0 + C1, 3, 3, seed=382, scale=1 / math.sqrt((C0 + C1) * 9))
+    b = _r(Co, seed=383)
+    temb = _r(N, Co, seed=384) if extra else None
+    res = _r(N, H, W, Co, seed=385) if extra else None
+    got = O.conv2d(_dev(x0.permute(0, 2, 3, 1), dt, device), w.to(dt).float(), b,
+                   x1=_dev(x1.permute(0, 2, 3, 1), dt, device) if C1 else None,
+                   rowadd=temb.to(device).contiguous() if extra else None,
+                   residual=_dev(res, dt, device) if extra else None)
+    xin = torch.cat([_q(x0, dt)] + ([_q(x1, dt)] if C1 else []), 1)
+    ref = F.conv2d(xin, _q(w, dt), b, padding=1)
+    if extra:
+        ref = ref + temb[:, :, None, None]
+    ref = ref.permute(0, 2, 3, 1)
+    if extra:
+        ref = ref + _q(res, dt)
+    assert O.rel_err(got, ref) < TOL[dt]
+    # every pixel, not only the norm: the strip seams and the image border are where a mapping slip would show
+    err = (got.float().cpu() - ref).abs().amax(dim=-1)
+    assert float(err.max()) < 0.05 * float(ref.abs().max()), err.argmax()
+
+
+@pytest.mark.parametrize("case", [
+    # (N, H, W, C0, C1, Cout): whole-row halo shapes also run as strips (halo_strip 2): same MFMAs per accumulator
+    (2, 64, 64, 320, 0, 320),
+    (1, 32, 64, 128, 0, 128),
+    (2, 16, 32, 128, 64, 160),
+    (16, 32, 32, 640, 0, 640),
+])
+@pytest.mark.parametrize("dt", DT16)
+def test_conv_halo_strip_equals_rows_bit_exact(device, case, dt):
+    """The strip tiles accumulate every output over the same (slab, tap, sub-step) order as the whole-row tiles, so
+    at W <= 64 forcing strips (option halo_strip 2) reproduces the row tiles bit for bit, residual and row add
+    included: the strip halo (neighbouring columns, zero borders) and the row mapping are exact."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    N, H, W, C0, C1, Co = case
+    x0 = _dev(_r(N, H, W, C0, seed=480), dt, device)
+    x1 = _dev(_r(N, H, W, C1, seed=481), dt, device) if C1 else None
+    w = _r(Co, C0 + C1, 3, 3, seed=482, scale=1 / math.sqrt((C0 + C1) * 9))
+    b = _r(Co, seed=483)
+    temb = _r(N, Co, seed=484).to(device).contiguous()
+    res = _dev(_r(N, H, W, Co, seed=485), dt, device)
+    L.call("irx_set_option", b"conv_halo", 2)
+    try:
+        outs = []
+        for strip in (1, 2):
+            L.call("irx_set_option", b"halo_strip", strip)
+            outs.append(O.conv2d(x0, w.to(dt).float(), b, x1=x1, rowadd=temb, residual=res))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1])
+    finally:
+        L.call("irx_set_option", b"halo_strip", 1)
+        L.call("irx_set_option", b"conv_halo", 1)
