@@ -94,6 +94,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gemm_nmajor", &g_gemm_nmajor, nullptr},
     {"halo_group", &g_halo_group, nullptr},
     {"halo_strip", &g_halo_strip, nullptr},
+    {"halo_up2", &g_halo_up2, nullptr},
     {"prof_shapes", &g_prof_shapes, nullptr},
     {"attn_prio", &g_attn_prio, nullptr},
     {"attn_qrep", &g_attn_qrep, nullptr},

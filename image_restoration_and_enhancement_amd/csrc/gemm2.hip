@@ -129,7 +129,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   // that are no power of two): the tile's GEMM rows are the strip's pixels in (row, column) order (host: the
   // tiles of an image are its strips, row block major), the halo is 10 rows x 32 columns plus the two
   // neighbouring columns (kept in the halo buffer's spare pixel rows), and the epilogue maps rows to NHWC pixels
-  constexpr bool STRIP = HALO == 5;
+  // HALO == 6 / 7: the per-parity 2x2 convs of a nearest-2x upsampler (GemmArgs::up2_*) on row / strip halo tiles:
+  // 4 taps per slab, (ky, kx) = (1 - pad_t + i, 1 - pad_l + j) of the 3x3 halo neighbourhood
+  constexpr bool STRIP = HALO == 5 || HALO == 7;
+  constexpr int NTAP = (HALO == 6 || HALO == 7) ? 4 : 9;
   constexpr int HB_U4 = (BM + 2 * kHaloWMax) * CPR;   // one halo slab buffer (uint4)
   constexpr int RING = HALO ? 2 * HB_U4 + S * BN * CPR + CPR + 64 : S * STAGE;
   // (+ a scratch KiB for the surplus DMA pieces, inside the epilogue's staging area when the ring is smaller)
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     }
   };
 
-  if constexpr (HALO == 2 || HALO == 4 || HALO == 5) {
+  if constexpr (HALO == 2 || HALO == 4 || HALO >= 5) {
     // ---- ping-pong halo main loop (the default halo path; no GroupNorm-fused operand).  The two waves that
     //      share a SIMD (w and w + 4) take opposite roles in each half of a K step (slab c = kt / 9, tap
     //      t = kt % 9), so one of them always has MFMAs to issue while the other moves data:
@@ -342,7 +345,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     const int nhi = (((BM >> lw) + 2) << lw) / RPI;   // halo wave-instructions (RPI pixel rows each)
     constexpr int NG = NW / 2;                        // waves per group
     constexpr int HPG = (BM + 2 * kHaloWMax) / RPI / NG;   // halo pieces per group-0 wave per slab
-    constexpr int HPARTS = 6, HPP = HPG / HPARTS;          // ... issued in 6 parts
+    // ... issued in 6 parts at taps 0-5 (4 taps per slab: 2 parts at taps 0-1), waited for at the slab's last tap
+    constexpr int HPARTS = NTAP == 9 ? 6 : 2, HPP = HPG / HPARTS;
     static_assert(HPG * RPI * NG == BM + 2 * kHaloWMax && HPP * HPARTS == HPG, "halo pieces");
     constexpr int NBI = BN / RPI, BPG = NBI / NG;          // B wave-instructions per step, per group-1 wave
     static_assert(BPG * NG == NBI, "B pieces");
@@ -431,11 +435,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     //      immediate.  The A swizzle of halo row hp is hp & 7 = (frow + kx - 1) & 7 (W and i * 16 are
     //      multiples of 8).
     int aoff[3][KSUB], boff[KSUB];
+    // NTAP == 4: the parity's tap offsets (block-uniform); aoff[0 / 1] = columns kx0 / kx0 + 1
+    const int ky0 = 1 - a.g.pad_t, kx0 = 1 - a.g.pad_l;
 #pragma unroll
     for (int ss = 0; ss < KSUB; ++ss) {
       const int ck = ss * 4 + fgrp;
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) aoff[kx][ss] = frow * CPR + (ck ^ ((frow + kx - 1) & 7));
+      for (int kx = 0; kx < 3; ++kx)
+        aoff[kx][ss] = frow * CPR + (ck ^ ((frow + (NTAP == 9 ? kx : kx0 + kx) - 1) & 7));
       boff[ss] = frow * CPR + (ck ^ (frow & 7));
     }
     const int awave = wm * TM * 16 * CPR, bwave = wn * TN * 16 * CPR, rowW = Wl * CPR;
@@ -443,8 +450,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int rx = (wm * TM * 16 + i * 16 + frow) & (Wl - 1);
-      zl[i] = rx == 0;
-      zr[i] = rx == Wl - 1;
+      zl[i] = rx == 0 && (NTAP == 9 || kx0 == 0);        // (NTAP 4: only a parity whose taps reach kx = 0 / 2)
+      zr[i] = rx == Wl - 1 && (NTAP == 9 || kx0 == 1);
     }
     // STRIP: the strip row of fragment i (its 16 rows lie in one 32-pixel strip row: wave-uniform); its edge lanes
     // read the neighbouring column's pixel of halo row eh + ky, logical chunk ck at slot ck ^ ((eh + ky) & 7)
@@ -452,8 +459,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
     for (int i = 0; i < TM; ++i) eh[i] = __builtin_amdgcn_readfirstlane((wm * TM * 16 + i * 16) >> lw);
     uint4 fa[KSUB][TM], fb[KSUB][TN];
-    auto readF = [&](auto tc, const uint4* Hs) {   // this wave's fragments of tap t (both 32-deep sub-steps)
-      constexpr int t = decltype(tc)::value, ky = t / 3, kx = t % 3, st = t % S;
+    // fragments of tap t (both 32-deep sub-steps), B from stage st.  NTAP 9: (ky, kx) = (t / 3, t % 3), st = t % 3,
+    // all compile-time; NTAP 4: ky = ky0 + t / 2 and column kx0 + t % 2 (block-uniform), the stage counted at run time
+    auto readF = [&](auto tc, const uint4* Hs, int st) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int kxi = NTAP == 9 ? t % 3 : t % 2;            // aoff column
+      constexpr int kxe = NTAP == 9 ? t % 3 : 2 * (t % 2);      // edge side: 0 left, 2 right, 1 none
+      const int ky = NTAP == 9 ? t / 3 : ky0 + t / 2;
+      const int kx = NTAP == 9 ? t % 3 : kx0 + t % 2;
       if (DG && (dbg & 16)) return;
       const uint4* Bs = Bsm + st * BN * CPR + bwave;
       const uint4* Hrow = Hs + awave + ky * rowW + (kx - 1) * CPR;
@@ -461,16 +474,16 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       for (int ss = 0; ss < KSUB; ++ss) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const uint4* src = Hrow + aoff[kx][ss] + i * 16 * CPR;
+          const uint4* src = Hrow + aoff[kxi][ss] + i * 16 * CPR;
           if constexpr (STRIP) {
-            if constexpr (kx != 1) {
+            if constexpr (kxe != 1) {
               const int h = eh[i] + ky;
-              const uint4* e = Hs + ((kx == 0 ? kStripEdgeL : kStripEdgeR) + h) * CPR + ((ss * 4 + fgrp) ^ (h & 7));
-              src = (kx == 0 ? zl[i] : zr[i]) ? e : src;
+              const uint4* e = Hs + ((kxe == 0 ? kStripEdgeL : kStripEdgeR) + h) * CPR + ((ss * 4 + fgrp) ^ (h & 7));
+              src = (kxe == 0 ? zl[i] : zr[i]) ? e : src;
             }
           } else {
-            if constexpr (kx == 0) src = zl[i] ? zrow + ss * 4 + fgrp : src;
-            if constexpr (kx == 2) src = zr[i] ? zrow + ss * 4 + fgrp : src;
+            if constexpr (kxe == 0) src = zl[i] ? zrow + ss * 4 + fgrp : src;
+            if constexpr (kxe == 2) src = zr[i] ? zrow + ss * 4 + fgrp : src;
           }
           fa[ss][i] = *src;
         }
@@ -521,8 +534,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #else
 #define IRX_STAMP(i)
 #endif
-    // this split's K steps [kt0, kt1): whole slabs (host: sp.per is a multiple of 9); >= 9 steps per split
-    const int c0 = kt0 / 9, cend = (kt1 + 8) / 9;
+    // this split's K steps [kt0, kt1): whole slabs (host: sp.per is a multiple of NTAP); >= NTAP steps per split.
+    // B stage of step kt: (kt - kt0) % 3 (= t % 3 at 9 taps per slab)
+    const int c0 = kt0 / NTAP, cend = (kt1 + NTAP - 1) / NTAP;
+    auto st_next = [](int st) { return st == S - 1 ? 0 : st + 1; };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     if (g1) {
@@ -531,42 +546,47 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       wait_vm(BPG);                                      // B(kt0) landed
       barrier();                                         // (+ the zero row, the zeroed out-of-image halo rows)
       barrier();                                         // group 1 runs one phase behind group 0
+      int sti = 0;                                       // (NTAP 4: the run-time stage of step kt)
       for (int c = c0; c < cend; ++c) {
         const uint4* Hs = Hb + (c & 1) * HB_U4;
-        static_for(std::make_integer_sequence<int, 9>{}, [&](auto tc) {
+        static_for(std::make_integer_sequence<int, NTAP>{}, [&](auto tc) {
           constexpr int t = decltype(tc)::value;
+          const int st = NTAP == 9 ? t % S : sti, st2 = NTAP == 9 ? (t + 2) % S : st_next(st_next(sti));
           // load phase: B(kt + 2) (past the split's end: a dummy), fragments of kt, B(kt + 1) landed
           // (fragment reads first: they are what this phase waits for; the DMA issue overlaps their latency)
           IRX_STAMP(0);
           prio(true);
-          readF(tc, Hs);
-          if constexpr (t < 7) issueB(c, std::integral_constant<int, t + 2>{}, (t + 2) % S);
-          else issueB(c + 1, std::integral_constant<int, t - 7>{}, (t + 2) % S);
+          readF(tc, Hs, st);
+          if constexpr (t < NTAP - 2) issueB(c, std::integral_constant<int, t + 2>{}, st2);
+          else issueB(c + 1, std::integral_constant<int, t + 2 - NTAP>{}, st2);
           IRX_STAMP(1);
           wait_vm(BPG);
           IRX_STAMP(2);
-          barrier(t == 8);
+          barrier(t == NTAP - 1);
           IRX_STAMP(3);
           prio(false);
           mma();                                         // compute phase
           IRX_STAMP(4);
           barrier();
           IRX_STAMP(5);
+          if constexpr (NTAP != 9) sti = st_next(sti);
         });
       }
     } else {
       issueH(c0, 0, HPG);
       wait_vm(0);                                        // H(c0) landed
       barrier();
+      int sti = 0;
       for (int c = c0; c < cend; ++c) {
         const uint4* Hs = Hb + (c & 1) * HB_U4;
         const bool more = c + 1 < cend;
-        static_for(std::make_integer_sequence<int, 9>{}, [&](auto tc) {
+        static_for(std::make_integer_sequence<int, NTAP>{}, [&](auto tc) {
           constexpr int t = decltype(tc)::value;
-          // load phase: a sixth of slab c + 1's halo, fragments of kt (B(kt) landed: group 1 waited for it)
+          const int st = NTAP == 9 ? t % S : sti;
+          // load phase: a part of slab c + 1's halo, fragments of kt (B(kt) landed: group 1 waited for it)
           IRX_STAMP(0);
           prio(true);
-          readF(tc, Hs);
+          readF(tc, Hs, st);
           if constexpr (t < HPARTS) {
             if (more) issueH(c + 1, t * HPP, (t + 1) * HPP);
           }
@@ -576,10 +596,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
           IRX_STAMP(3);
           prio(false);
           mma();                                         // compute phase
-          if constexpr (t == 8) wait_vm(0);              // slab c + 1's halo landed
+          if constexpr (t == NTAP - 1) wait_vm(0);       // slab c + 1's halo landed
           IRX_STAMP(4);
           barrier();
           IRX_STAMP(5);
+          if constexpr (NTAP != 9) sti = st_next(sti);
         });
       }
       barrier();
@@ -1746,8 +1767,9 @@ int gemm_emits_gn_parts(const GemmArgs& a) {
 bool gemm_up2_ok(const GemmArgs& a) {
   // every store of the large-tile path goes through c_off (the 16-byte epilogue, the split-K reduce kernel); the
   // scalar epilogue and the 4-wave kernel do not map rows
-  return g_large_tiles && eligible(a) && vec_ok(a) && !halo_bn(a) && !gemm_sk_eligible(a) && a.batch == 1 &&
-         !a.hs_L && choose(a).BM != 0;
+  // (the halo parity convs, HALO == 6 / 7, store through c_off too)
+  return g_large_tiles && eligible(a) && vec_ok(a) && a.batch == 1 && !a.hs_L &&
+         (halo_bn(a) || (!gemm_sk_eligible(a) && choose(a).BM != 0));
 }
 
 int g_ln_fold = 1;
@@ -1882,13 +1904,21 @@ int halo_splits(const GemmArgs& a, long tiles) {
 // tiles where whole-row tiles do not fit (W > 64 or no power of two), 2 strip tiles wherever the shape allows (tests:
 // strips == rows bit for bit at W <= 64)
 int g_halo_strip = 1;
+int g_halo_up2 = 1;   // irx_set_option("halo_up2", 0): upsampler parity convs on the im2col walk (A/B)
 
-// Halo tile mode of a 3x3 / stride-1 / pad-1 conv: 1 = 256-pixel tiles of whole image rows (W in {16, 32, 64}),
-// 2 = 8 x 32 strip tiles (W % 32 == 0, H % 8 == 0; HALO == 5), 0 = neither
+// Halo tile mode of a 3x3 / stride-1 / pad-1 conv, or of one parity's 2x2 conv of a nearest-2x upsampler
+// (GemmArgs::up2_*, pad (1 - a, 1 - b)): 1 = 256-pixel tiles of whole image rows (W in {16, 32, 64}), 2 = 8 x 32
+// strip tiles (W % 32 == 0, H % 8 == 0; HALO == 5 / 7), 0 = neither.  The decision does not depend on the parity.
 int halo_mode(const GemmArgs& a) {
   const ConvGeom& g = a.g;
   if (!g_conv_halo || !a.conv || a.batch != 1 || a.geglu || a.out_f32 || !vec_ok(a)) return 0;
-  if (g.KH != 3 || g.KW != 3 || g.stride != 1 || g.pad_t != 1 || g.pad_l != 1) return 0;
+  if (g.stride != 1) return 0;
+  if (a.up2_w) {   // (ping-pong loop only; whole 256-row tiles of one image: the sub-pixel GroupNorm partial blocks)
+    if (!g_halo_up2 || !g_halo_pipe || a.gn_ab || g.KH != 2 || g.KW != 2 || (g.pad_t & ~1) || (g.pad_l & ~1)) return 0;
+    if (((long)a.up2_h * a.up2_w) % 256) return 0;
+  } else if (g.KH != 3 || g.KW != 3 || g.pad_t != 1 || g.pad_l != 1) {
+    return 0;
+  }
   if (g.Hv != g.Hin || g.Wv != g.Win || g.Ho != g.Hin || g.Wo != g.Win) return 0;
   if (g.C0 % 64 || g.C1 % 64 || g.C0 <= 0) return 0;
   const int W = g.Win;
@@ -1907,6 +1937,7 @@ int halo_bn(const GemmArgs& a) {
   if (!mode) return 0;
   const int bn = a.N % 160 == 0 ? 160 : (a.N % 128 == 0 && g_halo_pipe && !a.gn_ab) ? 128 : 0;
   if (!bn || !halo_splits(a, canon_rows(a) / 256 * (a.N / bn))) return 0;
+  if (a.up2_w && mode == 2 && bn != 128) return 0;   // (strip parity convs: the VAE widths only, HALO == 7 at BN 128)
   // (GroupNorm-fused operand: one 512-element chunk of the (256 + 2W) x 8 halo per tap, taps 3..8)
   static_assert((256 + 2 * kHaloWMax) * 8 <= 512 * 6, "halo normalisation chunks");
   return bn;
@@ -1929,10 +1960,11 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     Split sp;
     sp.per = a.K / 64;
     const int splits = halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));
+    const int ntap = a.up2_w ? 4 : 9;
     if (splits > 1) {   // whole slabs per split, in-kernel last-arriver reduction (fp32 partials)
       const int slabs = (a.g.C0 + a.g.C1) / 64;
       sp.splits = splits;
-      sp.per = 9 * ((slabs + splits - 1) / splits);
+      sp.per = ntap * ((slabs + splits - 1) / splits);
       sp.Mp = a.M;
       sp.Np = a.N;
       const size_t need = (size_t)splits * a.M * a.N * sizeof(float);
@@ -1944,7 +1976,11 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     if (g_halo_pipe && !a.gn_ab && b.dbg && a.dtype == BF16) launch2<256, 160, 4, 2, 64, 3, 4>(b, sp, s);   // (diagnostics)
     else
 #endif
-    if (halo_mode(a) == 2) {            // strip tiles (ping-pong main loop)
+    if (a.up2_w) {                      // upsampler parity convs: 4 taps per slab
+      if (halo_mode(a) == 2) launch2<256, 128, 4, 2, 64, 3, 7>(b, sp, s);
+      else if (hbn == 160) launch2<256, 160, 4, 2, 64, 3, 6>(b, sp, s);
+      else launch2<256, 128, 4, 2, 64, 3, 6>(b, sp, s);
+    } else if (halo_mode(a) == 2) {     // strip tiles (ping-pong main loop)
       if (hbn == 160) launch2<256, 160, 4, 2, 64, 3, 5>(b, sp, s);
       else launch2<256, 128, 4, 2, 64, 3, 5>(b, sp, s);
     } else if (g_halo_pipe && !a.gn_ab) {   // ping-pong main loop

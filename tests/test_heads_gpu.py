@@ -283,3 +283,43 @@ def test_unet_reduce_kernel_groupnorm_partials(device, dtype):
     rel = float((a - b).norm() / b.norm())
     print(f"\nreduce-kernel GroupNorm partials vs stats pass ({dtype}): rel L2 {rel:.2e}")
     assert rel < (1e-2 if dtype == "bf16" else 2e-3), rel
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_halo_up2_vs_im2col_up2(device, dtype):
+    """The upsamplers' per-parity 2x2 convs on 4-tap halo tiles (option halo_up2, default: row tiles at low-resolution
+    widths 16 / 32 / 64, strip tiles at 128) vs the same convs on the im2col walk: the same products, summed slab-major
+    instead of tap-major, so the outputs agree to fp32 reassociation.  VAE decoder from 32x32 latents (up2 at
+    32 -> 64 and 64 -> 128 on row tiles, 128 -> 256 on strips) and the UNet at 64x64 (16 -> 32, 32 -> 64)."""
+    from tests import models_common as MC
+    from image_restoration_and_enhancement_amd.engine import UNet, VAE
+    pc, sd = MC.state_dicts("denoise")
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    g = torch.Generator().manual_seed(13)
+    vae = VAE(pc.vae, dtype, device)
+    vae.load_state_dict(sd["vae"])
+    z = torch.zeros(2, 32, 32, 8)
+    z[..., :4] = torch.randn(2, 32, 32, 4, generator=g)
+    z = z.to(tdt).to(device).contiguous()
+    outs = []
+    for v in (1, 0):
+        with L.option(halo_up2=v):
+            outs.append(vae.decode(z).float().cpu())
+    rel_vae = float((outs[0] - outs[1]).norm() / outs[1].norm())
+    unet = UNet(pc.unet, dtype, device)
+    unet.load_state_dict(sd["unet"])
+    xin = torch.zeros(2, 64, 64, unet.cin_pad)
+    xin[..., :4] = torch.randn(2, 64, 64, 4, generator=g)
+    xin = xin.to(tdt).to(device).contiguous()
+    kv = unet.prepare_context(torch.randn(2, 77, 768, generator=g).to(tdt).to(device).contiguous())
+    uo = []
+    for v in (1, 0):
+        with L.option(halo_up2=v):
+            uo.append(unet.forward(xin, torch.full((2,), 481.0, device=device), kv, 77).float().cpu())
+    rel_unet = float((uo[0] - uo[1]).norm() / uo[1].norm())
+    print(f"\nhalo up2 vs im2col up2 ({dtype}): VAE rel L2 {rel_vae:.2e}, UNet rel L2 {rel_unet:.2e}")
+    assert torch.isfinite(outs[0]).all() and torch.isfinite(uo[0]).all()
+    # (the bars of the up2-vs-resize tests above; measured round 6: VAE 1.5e-2 / 1.9e-3, UNet 7.9e-3 / 9.9e-4 for
+    # bf16 / fp16 — the 8x ratio of the two types' rounding, i.e. reassociation, not a mapping error)
+    assert rel_vae < (3e-2 if dtype == "bf16" else 5e-3), rel_vae
+    assert rel_unet < (2e-2 if dtype == "bf16" else 4e-3), rel_unet
