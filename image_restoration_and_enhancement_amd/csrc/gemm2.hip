@@ -776,12 +776,17 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const bool g1 = wv >= NW / 2;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)smem);
+    // two-source A (GemmArgs::A1, the 1x1 convs over a channel concat: proj_out o ff.net.2): A pieces switch to
+    // the second source's row base / lane offset (pb1 / pv1) from K = kA1 on (a block-uniform choice per step)
     const char* pb[IPW];
-    uint32_t pv[IPW], pd[IPW];
+    const char* pb1[IPW];
+    uint32_t pv[IPW], pv1[IPW], pd[IPW];
+    bool apc[IPW];
 #pragma unroll
     for (int j = 0; j < IPW; ++j) {
       const int q = wv * IPW + j, r0 = RPI * q, r = r0 + lrow;
       const int ch = (lslot ^ swz(r)) * 8;
+      apc[j] = q < NINST && r0 < BM;
       if (q < NINST && r0 < BM) {
         pb[j] = (const char*)(Ap + (long)(m0 + r0) * a.lda);
         pv[j] = (uint32_t)(lrow * a.lda + ch) * 2u;
@@ -793,13 +798,24 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
         pv[j] = (uint32_t)lane * 16u;
       }
       pd[j] = q < NINST ? lds0 + (uint32_t)(q * 64) * 16u : lds0 + (uint32_t)(SMEM - 64) * 16u;
+      pb1[j] = pb[j];
+      pv1[j] = pv[j];
+      if (A1p && apc[j]) {
+        pb1[j] = (const char*)(A1p + (long)(m0 + r0) * a.lda1);
+        pv1[j] = (uint32_t)(lrow * a.lda1 + ch) * 2u;
+      }
     }
     auto issueP = [&](int kt, int st) {
       const long ko = (long)kt * BK * 2;
+      const bool second = A1p && kt * BK >= a.kA1;
+      const long ko1 = second ? ko - (long)a.kA1 * 2 : ko;   // (A pieces' K offset in their source)
       const uint32_t so = (uint32_t)(st * STAGE) * 16u;
 #pragma unroll
-      for (int j = 0; j < IPW; ++j)
-        glds16_s(pv[j], pb[j] + ko, wv * IPW + j < NINST ? pd[j] + so : pd[j]);
+      for (int j = 0; j < IPW; ++j) {
+        const uint32_t dst = wv * IPW + j < NINST ? pd[j] + so : pd[j];
+        if (apc[j] && second) glds16_s(pv1[j], pb1[j] + ko1, dst);
+        else glds16_s(pv[j], pb[j] + ko, dst);
+      }
     };
     uint4 fa[KSUB][TM], fb[KSUB][TN];
     auto readF = [&](auto stc) {
@@ -1772,6 +1788,8 @@ bool gemm_up2_ok(const GemmArgs& a) {
          (halo_bn(a) || (!gemm_sk_eligible(a) && choose(a).BM != 0));
 }
 
+int g_gemm_pp_chain = 1;   // irx_set_option("gemm_pp_chain", 0): the two-source 1x1 chains on the two-stage loop (A/B)
+
 int g_ln_fold = 1;
 
 bool gemm_ln_foldable(const GemmArgs& a) {
@@ -2026,9 +2044,13 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     if (c.BN == 160) launch2<128, 160, 2, 2, 64, 2>(b, sp, s);
     else launch2<128, 128, 2, 2, 64, 2>(b, sp, s);
   } else if (g_gemm_deep == 0 &&
-             !a.A1 &&   // (the lean dense ping-pong addresses one A source)
-             (g_gemm_pp == 1 || (g_gemm_pp >= 2 && !a.conv && c.BM == 256 && (c.BN == 256 || (g_gemm_pp == 3 && c.BN == 320)) &&
-                                 !a.ln_out && !a.b_rows)) &&
+             (!a.A1 || g_gemm_pp_chain) &&   // (two-source A: the lean dense form only, a.conv == 0)
+             (g_gemm_pp == 1 ||
+              (g_gemm_pp >= 2 && !a.conv && !a.ln_out && !a.b_rows &&
+               ((c.BM == 256 && (c.BN == 256 || (g_gemm_pp == 3 && c.BN == 320))) ||
+                // the long-K two-source 1x1 convs (proj_out o ff.net.2 over (h | g), K = 5C): the ping-pong loop pays
+                // where the K loop is long (unlike the K = 320 / 640 projections, which stay on the two-stage loop)
+                (a.A1 && g_gemm_pp_chain && c.BN == 320 && (c.BM == 256 || c.BM == 128) && a.K >= 1024)))) &&
              (a.conv || (a.M % c.BM == 0 && a.N % c.BN == 0))) {
     // ping-pong schedule: 3 stages (BK 32 where BK 64 would not fit); dense GEMMs on whole tiles only (the lean form)
     const int key = c.BM * 1000 + c.BN;

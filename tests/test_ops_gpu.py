@@ -831,3 +831,28 @@ def test_conv_halo_strip_equals_rows_bit_exact(device, case, dt):
     finally:
         L.call("irx_set_option", b"halo_strip", 1)
         L.call("irx_set_option", b"conv_halo", 1)
+
+
+@pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("N,H,W,C0,C1,Co", [
+    (16, 64, 64, 320, 1280, 320),     # proj_out o ff.net.2 at 64^2, batch 16: 256 x 320 tiles
+    (16, 32, 32, 640, 2560, 640),     # ... at 32^2: 128 x 320 tiles
+    (16, 16, 16, 1280, 5120, 1280),   # ... at 16^2: 128 x 320 tiles, two in-kernel K splits
+    (2, 32, 32, 640, 2560, 640),
+])
+def test_chain_pingpong_bit_exact(device, dt, N, H, W, C0, C1, Co):
+    """The two-source 1x1 chains on the lean dense ping-pong loop (option gemm_pp_chain, default) run the same 32-deep
+    MFMA steps in the same K order into every accumulator as the two-stage loop: identical outputs, residual and the
+    second A source's switch at K = C0 included."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    d0 = _dev(_r(N, H, W, C0, seed=190), dt, device)
+    d1 = _dev(_r(N, H, W, C1, seed=191), dt, device)
+    w = _r(Co, C0 + C1, 1, 1, seed=192, scale=1 / math.sqrt(C0 + C1))
+    b = _r(Co, seed=193)
+    dr = _dev(_r(N, H, W, Co, seed=194), dt, device)
+    outs = []
+    for v in (1, 0):
+        with L.option(gemm_pp_chain=v):
+            outs.append(O.conv2d(d0, w.to(dt).float(), b, pad=(0, 0), x1=d1, residual=dr))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
