@@ -95,6 +95,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"halo_group", &g_halo_group, nullptr},
     {"halo_strip", &g_halo_strip, nullptr},
     {"halo_up2", &g_halo_up2, nullptr},
+    {"halo_mi", &g_halo_mi, nullptr},
     {"gemm_pp_chain", &g_gemm_pp_chain, nullptr},
     {"prof_shapes", &g_prof_shapes, nullptr},
     {"attn_prio", &g_attn_prio, nullptr},

@@ -133,6 +133,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   // 4 taps per slab, (ky, kx) = (1 - pad_t + i, 1 - pad_l + j) of the 3x3 halo neighbourhood
   constexpr bool STRIP = HALO == 5 || HALO == 7;
   constexpr int NTAP = (HALO == 6 || HALO == 7) ? 4 : 9;
+  // HALO == 8: 8 x 8 images (the UNet's 8x8 level), four whole images per 256-row tile: image j's halo is its own
+  // 10 x 8 block at halo pixel 80 j (zero rows above / below, never DMA'd), so a tap of tile row r reads halo pixel
+  // r + 16 j + 8 ky + kx - 1; K splits finish in the separate reduce kernels (host)
+  constexpr bool MI = HALO == 8;
   constexpr int HB_U4 = (BM + 2 * kHaloWMax) * CPR;   // one halo slab buffer (uint4)
   constexpr int RING = HALO ? 2 * HB_U4 + S * BN * CPR + CPR + 64 : S * STAGE;
   // (+ a scratch KiB for the surplus DMA pieces, inside the epilogue's staging area when the ring is smaller)
@@ -334,15 +338,18 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     const int Wl = STRIP ? kStripW : W, lw = __builtin_ctz(Wl);   // pixels per halo row in LDS
     const int HW = H * W;
     const int img = m0 / HW;
-    int y0, x0 = 0;   // the tile's first output row / column
-    if constexpr (STRIP) {
+    int y0 = 0, x0 = 0;   // the tile's first output row / column
+    const int img0 = MI ? m0 >> 6 : 0, nimg = MI ? min(4, (a.M - m0) >> 6) : 0;   // (MI: images of the tile)
+    if constexpr (MI) {
+    } else if constexpr (STRIP) {
       const int t = (m0 - img * HW) / BM, ns = W / kStripW, rb = t / ns;
       y0 = rb * (BM / kStripW);
       x0 = (t - rb * ns) * kStripW;
     } else {
       y0 = (m0 - img * HW) >> lw;
     }
-    const int nhi = (((BM >> lw) + 2) << lw) / RPI;   // halo wave-instructions (RPI pixel rows each)
+    // halo wave-instructions (RPI pixel rows each; MI: the 4 images' 8 rows, the pad rows are zeroed instead)
+    const int nhi = MI ? 32 : (((BM >> lw) + 2) << lw) / RPI;
     constexpr int NG = NW / 2;                        // waves per group
     constexpr int HPG = (BM + 2 * kHaloWMax) / RPI / NG;   // halo pieces per group-0 wave per slab
     // ... issued in 6 parts at taps 0-5 (4 taps per slab: 2 parts at taps 0-1), waited for at the slab's last tap
@@ -363,7 +370,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     // lane -> (row lr of the piece's 8, 16-byte chunk slot); the slot holds logical chunk slot ^ lr (= row & 7)
     const int lr = lane >> 3, lch = (lane & 7) ^ lr;
     // ---- halo rows outside the image (top / bottom tiles): zero in both buffers once, never DMA'd
-    {
+    if constexpr (MI) {   // every image's pad rows 0 and 9 (8 pixels each), both buffers
+      for (int i = tid; i < 2 * 4 * 2 * 8 * CPR; i += NT) {
+        const int buf = i / (4 * 2 * 8 * CPR), rem = i - buf * (4 * 2 * 8 * CPR);
+        const int j = rem / (2 * 8 * CPR), side = (rem / (8 * CPR)) & 1, k = rem % (8 * CPR);
+        Hb[buf * HB_U4 + (j * 80 + side * 72) * CPR + k] = uint4{0u, 0u, 0u, 0u};
+      }
+    } else {
       const int ylo = y0 - 1, yhi = y0 + (BM >> lw);   // the halo's first / last image row
       for (int i = tid; i < 2 * (Wl * CPR); i += NT) {
         const int side = i / (Wl * CPR), k = i - side * (Wl * CPR);
@@ -408,6 +421,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
       for (int j = j0; j < j1; ++j) {
         const int q = gw * HPG + j;
+        if constexpr (MI) {   // piece q: image j = q / 8, its row q % 8 -> halo pixel 80 j + 8 + 8 (q % 8)
+          const int j = q >> 3;
+          const long P = (long)(img0 + j) * 64 + (q & 7) * RPI;
+          const bool ok = q < nhi && j < nimg;
+          glds16_s(vo, ok ? sb + (P * cs + ch) * 2 : sb, ok ? mb + (uint32_t)(j * 10 + 1 + (q & 7)) * 1024u : ldsX);
+          continue;
+        }
         if constexpr (STRIP) {
           if (q >= nhi && q < nhi + 4) {   // a neighbouring column: per-lane addresses (one pixel per lane row)
             const int e = q - nhi, hr = (e & 1) * RPI + lr, yy = y0 - 1 + hr;
@@ -458,6 +478,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     int eh[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) eh[i] = __builtin_amdgcn_readfirstlane((wm * TM * 16 + i * 16) >> lw);
+    // MI: fragment i's image j (its 16 rows lie in one 64-row image) shifts its halo reads by 16 j pixels
+    int mio[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) mio[i] = MI ? __builtin_amdgcn_readfirstlane(((wm * TM * 16 + i * 16) >> 6) * 16 * CPR) : 0;
     uint4 fa[KSUB][TM], fb[KSUB][TN];
     // fragments of tap t (both 32-deep sub-steps), B from stage st.  NTAP 9: (ky, kx) = (t / 3, t % 3), st = t % 3,
     // all compile-time; NTAP 4: ky = ky0 + t / 2 and column kx0 + t % 2 (block-uniform), the stage counted at run time
@@ -474,7 +498,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       for (int ss = 0; ss < KSUB; ++ss) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const uint4* src = Hrow + aoff[kxi][ss] + i * 16 * CPR;
+          const uint4* src = Hrow + aoff[kxi][ss] + i * 16 * CPR + mio[i];
           if constexpr (STRIP) {
             if constexpr (kxe != 1) {
               const int h = eh[i] + ky;
@@ -1737,6 +1761,7 @@ int g_gn_fuse = 0;   // measured slower: the halo normalisation's V
 int halo_bn(const GemmArgs& a);
 
 int halo_mode(const GemmArgs& a);
+int halo_split_count(const GemmArgs& a, int hbn);
 
 bool gemm_gn_fusable(const GemmArgs& a) {   // (the lock-step halo loop, HALO == 1: 160-wide row tiles only)
   return g_gn_fuse && g_large_tiles && is16(a.dtype) && eligible(a) && halo_bn(a) == 160 && halo_mode(a) == 1;
@@ -1765,7 +1790,12 @@ int g_gn_red_parts = 1;   // irx_set_option("gn_red_parts", 0): split-K reduce k
 int gemm_emits_gn_parts(const GemmArgs& a) {
   if (!g_gn_parts || !g_large_tiles || !is16(a.dtype) || !eligible(a) || !vec_ok(a)) return 0;
   if (a.geglu || a.hs_L || a.batch != 1 || a.out_f32) return 0;
-  if (halo_bn(a)) return a.M % 256 == 0 ? 256 : 0;
+  if (halo_bn(a)) {
+    if (halo_mode(a) == 3)   // (8x8 images, K splits reduced by splitk_reduce_gn_kernel: one partial per image)
+      return (g_gn_red_parts && halo_split_count(a, 160) > 1 && a.M % kRedGnRows == 0 && a.N % 64 == 0 && a.act == ACT_NONE && !a.b_rows) ? kRedGnRows
+                                                                                                            : 0;
+    return a.M % 256 == 0 ? 256 : 0;
+  }
   const Choice c = choose(a);
   if (c.BM == 0) return 0;
   if (c.splits > 1) {   // the in-kernel split-K reduction runs the epilogue; the separate reduce kernel emits them too
@@ -1841,7 +1871,7 @@ int halo_splits(const GemmArgs& a, long tiles);
 // K splits the large-tile path would run `a` with (1: none; 0: not a large-tile shape) — for tests / diagnostics
 int gemm_large_splits(const GemmArgs& a) {
   if (!g_large_tiles || !eligible(a) || gemm_sk_eligible(a)) return 0;
-  if (const int hbn = halo_bn(a)) return halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));
+  if (const int hbn = halo_bn(a)) return halo_split_count(a, hbn);
   const Choice c = choose(a);
   return c.BM ? c.splits : 0;
 }
@@ -1890,8 +1920,8 @@ int halo_group_m(const GemmArgs& a, int bn) {
 size_t gemm_workspace_bytes(const GemmArgs& a) {
   if (!g_large_tiles || !eligible(a)) return 0;
   if (const int hbn = halo_bn(a)) {
-    const int sp = halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));
-    return sp > 1 ? (size_t)sp * a.M * a.N * sizeof(float) : 0;
+    const int sp = halo_split_count(a, hbn);
+    return sp > 1 ? (size_t)sp * ((a.M + 255) / 256 * 256) * a.N * sizeof(float) : 0;
   }
   const Choice c = choose(a);
   if (c.BM == 0 || c.splits <= 1) return 0;
@@ -1923,6 +1953,7 @@ int halo_splits(const GemmArgs& a, long tiles) {
 // strips == rows bit for bit at W <= 64)
 int g_halo_strip = 1;
 int g_halo_up2 = 1;   // irx_set_option("halo_up2", 0): upsampler parity convs on the im2col walk (A/B)
+int g_halo_mi = 1;    // irx_set_option("halo_mi", 0): the 8x8-level convs on the im2col walk (A/B)
 
 // Halo tile mode of a 3x3 / stride-1 / pad-1 conv, or of one parity's 2x2 conv of a nearest-2x upsampler
 // (GemmArgs::up2_*, pad (1 - a, 1 - b)): 1 = 256-pixel tiles of whole image rows (W in {16, 32, 64}), 2 = 8 x 32
@@ -1940,7 +1971,11 @@ int halo_mode(const GemmArgs& a) {
   if (g.Hv != g.Hin || g.Wv != g.Win || g.Ho != g.Hin || g.Wo != g.Win) return 0;
   if (g.C0 % 64 || g.C1 % 64 || g.C0 <= 0) return 0;
   const int W = g.Win;
-  if ((long)g.N * g.Hin * W != a.M || a.M % 256) return 0;
+  if ((long)g.N * g.Hin * W != a.M) return 0;
+  // 3 = four whole 8x8 images per tile (HALO == 8): any image count (a partial last tile), so the choice is
+  // batch-invariant like the others
+  if (W == 8 && g.Hin == 8 && !a.up2_w && g_halo_mi && g_halo_pipe && !a.gn_ab && a.M % 64 == 0) return 3;
+  if (a.M % 256) return 0;
   const bool rows = W >= 16 && W <= kHaloWMax && !(W & (W - 1)) && 256 % W == 0 && g.Hin % (256 / W) == 0;
   // (strips: the ping-pong loop only, no GroupNorm-fused operand)
   const bool strips = g_halo_strip && g_halo_pipe && !a.gn_ab && W % kStripW == 0 && g.Hin % (256 / kStripW) == 0;
@@ -1954,11 +1989,23 @@ int halo_bn(const GemmArgs& a) {
   const int mode = halo_mode(a);
   if (!mode) return 0;
   const int bn = a.N % 160 == 0 ? 160 : (a.N % 128 == 0 && g_halo_pipe && !a.gn_ab) ? 128 : 0;
+  if (mode == 3) return bn == 160 ? 160 : 0;   // (HALO == 8 instantiated at BN 160: the UNet's 1280 channels)
   if (!bn || !halo_splits(a, canon_rows(a) / 256 * (a.N / bn))) return 0;
   if (a.up2_w && mode == 2 && bn != 128) return 0;   // (strip parity convs: the VAE widths only, HALO == 7 at BN 128)
   // (GroupNorm-fused operand: one 512-element chunk of the (256 + 2W) x 8 halo per tap, taps 3..8)
   static_assert((256 + 2 * kHaloWMax) * 8 <= 512 * 6, "halo normalisation chunks");
   return bn;
+}
+
+// K splits of a halo conv: halo_splits (1 or 2, in-kernel reduction), or for the 8x8 images (mode 3) whole slabs per
+// split for about one block per CU (the canonical 16 images: 4 row tiles x N / 160), reduced by the separate kernel
+int halo_split_count(const GemmArgs& a, int hbn) {
+  if (halo_mode(a) != 3) return halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));
+  const long tiles = (canon_rows(a) + 255) / 256 * (a.N / hbn);
+  const int slabs = (a.g.C0 + a.g.C1) / 64;
+  const int want = (int)std::max(1L, std::min(8L, (long)kCUs / std::max(1L, tiles)));
+  const int per = (slabs + want - 1) / want;
+  return (slabs + per - 1) / per;
 }
 
 // Returns false (caller uses the 4-wave kernel) when the shape does not fit the large-tile path.
@@ -1977,24 +2024,27 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     b.group_m = halo_group_m(a, hbn);
     Split sp;
     sp.per = a.K / 64;
-    const int splits = halo_splits(a, canon_rows(a) / 256 * (a.N / hbn));
+    const int splits = halo_split_count(a, hbn);
     const int ntap = a.up2_w ? 4 : 9;
-    if (splits > 1) {   // whole slabs per split, in-kernel last-arriver reduction (fp32 partials)
+    const bool mi = halo_mode(a) == 3;
+    if (splits > 1) {   // whole slabs per split, in-kernel last-arriver reduction (fp32 partials; 8x8: reduce kernel)
       const int slabs = (a.g.C0 + a.g.C1) / 64;
       sp.splits = splits;
       sp.per = ntap * ((slabs + splits - 1) / splits);
-      sp.Mp = a.M;
+      sp.Mp = (a.M + 255) / 256 * 256;   // (whole row tiles of partials: a partial last tile stores all its rows)
       sp.Np = a.N;
-      const size_t need = (size_t)splits * a.M * a.N * sizeof(float);
+      const size_t need = (size_t)splits * sp.Mp * a.N * sizeof(float);
       sp.ws = (a.splitk_ws && a.splitk_ws_bytes >= need) ? (float*)a.splitk_ws : internal_ws(need);
-      sp.inkernel = true;
-      sp.cnt = stream_counters(s);
+      sp.inkernel = !mi;
+      if (sp.inkernel) sp.cnt = stream_counters(s);
     }
 #ifdef IRX_HALO_DIAG
     if (g_halo_pipe && !a.gn_ab && b.dbg && a.dtype == BF16) launch2<256, 160, 4, 2, 64, 3, 4>(b, sp, s);   // (diagnostics)
     else
 #endif
-    if (a.up2_w) {                      // upsampler parity convs: 4 taps per slab
+    if (mi) {                           // four 8x8 images per tile
+      launch2<256, 160, 4, 2, 64, 3, 8>(b, sp, s);
+    } else if (a.up2_w) {               // upsampler parity convs: 4 taps per slab
       if (halo_mode(a) == 2) launch2<256, 128, 4, 2, 64, 3, 7>(b, sp, s);
       else if (hbn == 160) launch2<256, 160, 4, 2, 64, 3, 6>(b, sp, s);
       else launch2<256, 128, 4, 2, 64, 3, 6>(b, sp, s);

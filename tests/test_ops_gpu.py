@@ -856,3 +856,45 @@ def test_chain_pingpong_bit_exact(device, dt, N, H, W, C0, C1, Co):
             outs.append(O.conv2d(d0, w.to(dt).float(), b, pad=(0, 0), x1=d1, residual=dr))
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("case", [
+    # (N, C0, C1, Cout, rowadd+residual): the UNet's 8x8-level convs (four images per halo tile, K splits + the
+    # reduce kernel), a partial last tile (N % 4 != 0), the up-block concat
+    (16, 1280, 0, 1280, True),
+    (5, 1280, 0, 1280, False),
+    (3, 1280, 1280, 1280, True),
+    (16, 640, 640, 1280, True),
+])
+@pytest.mark.parametrize("dt", DT16)
+def test_conv_halo_8x8_images(device, case, dt):
+    """3x3 convs over 8x8 images on four-image halo tiles (HALO == 8, option halo_mi): each image's halo block with its
+    own zero pad rows, split-K partials reduced by the separate kernel; vs the fp32 CPU conv, and vs the im2col walk
+    (halo_mi 0) within the reassociation of a different K order."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    N, C0, C1, Co, extra = case
+    x0 = _r(N, C0, 8, 8, seed=580)
+    x1 = _r(N, C1, 8, 8, seed=581) if C1 else None
+    w = _r(Co, C0 + C1, 3, 3, seed=582, scale=1 / math.sqrt((C0 + C1) * 9))
+    b = _r(Co, seed=583)
+    temb = _r(N, Co, seed=584) if extra else None
+    res = _r(N, 8, 8, Co, seed=585) if extra else None
+    args = dict(x1=_dev(x1.permute(0, 2, 3, 1), dt, device) if C1 else None,
+                rowadd=temb.to(device).contiguous() if extra else None,
+                residual=_dev(res, dt, device) if extra else None)
+    d0 = _dev(x0.permute(0, 2, 3, 1), dt, device)
+    got = O.conv2d(d0, w.to(dt).float(), b, **args)
+    with L.option(halo_mi=0):
+        walk = O.conv2d(d0, w.to(dt).float(), b, **args)
+    xin = torch.cat([_q(x0, dt)] + ([_q(x1, dt)] if C1 else []), 1)
+    ref = F.conv2d(xin, _q(w, dt), b, padding=1)
+    if extra:
+        ref = ref + temb[:, :, None, None]
+    ref = ref.permute(0, 2, 3, 1)
+    if extra:
+        ref = ref + _q(res, dt)
+    assert O.rel_err(got, ref) < TOL[dt]
+    # (two K orders, each rounded once to the 16-bit output: about one bf16 ulp apart on some elements)
+    assert O.rel_err(got, walk.float()) < (8e-3 if dt == torch.bfloat16 else 2e-3)
+    err = (got.float().cpu() - ref).abs().amax(dim=-1)   # every pixel: image seams and pad rows
+    assert float(err.max()) < 0.05 * float(ref.abs().max()), err.argmax()
