@@ -234,8 +234,14 @@ void launch_cfg(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, a.batch), block(kThreads);
-  ProfScope ps(prof_on() ? kname<T, WM, WN, TM, TN>(a.conv, a.out_f32) : std::string(),
-               2.0 * a.M * a.N * (double)a.K * a.batch, s);
+  std::string nm;
+  if (prof_on()) {
+    nm = kname<T, WM, WN, TM, TN>(a.conv, a.out_f32);
+    if (g_prof_shapes)
+      nm += " [M " + std::to_string(a.M) + " N " + std::to_string(a.N) + " K " + std::to_string(a.K) + " batch " +
+            std::to_string(a.batch) + (a.hs_L ? " hs" : "") + (a.residual ? " res" : "") + "]";
+  }
+  ProfScope ps(nm, 2.0 * a.M * a.N * (double)a.K * a.batch, s);
   if (a.hs_L) {
     IRX_CHECK(!a.conv && !a.out_f32, "head-split output: plain 16-bit GEMMs only");
     gemm_kernel<T, WM, WN, TM, TN, false, false, true><<<grid, block, 0, s>>>(a);

@@ -1917,6 +1917,33 @@ int halo_group_m(const GemmArgs& a, int bn) {
   return best < 0.9 * legacy ? (int)best_g : 0;
 }
 
+// Tile order of a dense large-tile GEMM (scheduling only): the cost model of halo_group_m with A panel BM x K and B
+// panel BN x K, over the 32 x `resident` tiles one XCD runs at once; 0 keeps the M-major / N-major order when the
+// grouped one is not > 10 % better.  (The GEGLU projections at 32^2 / 16^2: every XCD streamed the whole 6.5 / 26 MB
+// weight in the M-major / N-major orders.)
+int g_gemm_group = 1;   // irx_set_option("gemm_group", 0): the M-major / N-major dense tile orders only (A/B)
+int dense_group_m(const GemmArgs& a, int bm, int bn, int resident, bool nmajor) {
+  if (!g_gemm_group) return 0;
+  const long tiles_m = (a.M + bm - 1) / bm, tiles_n = (a.N + bn - 1) / bn;
+  if (tiles_n < 2 || tiles_m < 2) return 0;
+  const long q = (tiles_m * tiles_n + 7) / 8, w = std::min(q, 32L * resident);
+  const double a_m = (double)bm * a.K * 2.0, b_n = (double)bn * a.K * 2.0;
+  auto cost = [&](long g) {
+    const bool whole = w >= g * tiles_n;
+    const long gm = whole ? (w + tiles_n - 1) / tiles_n : std::min(g, w);
+    const long gn = whole ? tiles_n : (w + g - 1) / g;
+    return gm * a_m + gn * b_n;
+  };
+  // the current order: M-major = groups of one whole M row block; N-major = a window of w M tiles x w / tiles_m N tiles
+  const double legacy = nmajor ? std::min(w, tiles_m) * a_m + (double)((w + tiles_m - 1) / tiles_m) * b_n
+                               : cost(std::max(1L, (w + tiles_n - 1) / tiles_n));
+  long best_g = 0;
+  double best = legacy;
+  for (long g = 1; g <= tiles_m; g *= 2)
+    if (cost(g) < best) { best = cost(g); best_g = g; }
+  return best < 0.9 * legacy ? (int)best_g : 0;
+}
+
 size_t gemm_workspace_bytes(const GemmArgs& a) {
   if (!g_large_tiles || !eligible(a)) return 0;
   if (const int hbn = halo_bn(a)) {
@@ -2067,6 +2094,10 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
   // tile order (scheduling only, no numeric effect): N-major when the weights outweigh the activation rows, so that an
   // XCD's consecutive tiles re-use one B panel from its L2 instead of every XCD streaming all of B
   b.nmajor = g_gemm_nmajor == 2 || (g_gemm_nmajor == 1 && (long)a.N * a.batch > (long)a.M * a.batch);
+  if (a.batch == 1 && !a.hs_L) {   // grouped order where it cuts an XCD's co-resident A + B bytes (GemmArgs::group_m)
+    b.group_m = dense_group_m(a, c.BM, c.BN, (c.BM == 128 && c.BN == 128) || c.small ? 2 : 1, b.nmajor);
+    if (b.group_m) b.nmajor = 0;
+  }
   if (a.geglu && !b.vec_epilogue) return false;
   Split sp;
   sp.splits = c.splits;

@@ -173,6 +173,7 @@ extern bool g_large_tiles;
 extern int g_large_mask;
 extern int g_large_dense;
 extern int g_gemm_pp_chain;   // 1 (default): the long-K two-source 1x1 chains on the lean dense ping-pong loop
+extern int g_gemm_group;   // 1 (default): grouped dense tile order where it cuts per-XCD A + B bytes by > 10 %
 extern int g_halo_mi;      // 1 (default): the 8x8-level 3x3 convs on 4-image halo tiles (K splits, reduce kernel)
 extern int g_halo_up2;     // 1 (default): upsampler parity convs (2x2, GemmArgs::up2_*) on 4-tap halo tiles
 extern int g_halo_strip;   // 1 (default): 8 x 32 strip halo tiles where whole-row tiles do not fit; 2 wherever allowed
