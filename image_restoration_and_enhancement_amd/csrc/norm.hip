@@ -335,13 +335,19 @@ __global__ __launch_bounds__(256) void gn_fa_kernel(const double2* __restrict__ 
   }
   __syncthreads();
   const int nch = nc / VEC, tot = np * nch;
-  auto src_of = [&](int idx, int& k) -> const T* {
-    const int pp = idx / nch, p = plo + pp;
-    k = idx - pp * nch;
-    const int c = c0 + k * VEC;
+  // chunk idx = pp * nch + k (pixel pp of the slice, 16-byte channel chunk k): each thread steps idx by 256, i.e.
+  // (pp, k) by (256 / nch, 256 % nch) with one carry — no integer division per chunk (nch <= 32: nc <= 256)
+  const int dp = 256 / nch, dk = 256 - dp * nch;
+  auto adv = [&](int& pp, int& k) {
+    pp += dp;
+    k += dk;
+    if (k >= nch) { k -= nch; ++pp; }
+  };
+  auto src_at = [&](int pp, int k) -> const T* {
+    const int p = plo + pp, c = c0 + k * VEC;
     return c < C0 ? x0 + ((long)n * HW + p) * C0 + c : x1 + ((long)n * HW + p) * C1 + (c - C0);
   };
-  auto one = [&](const uint4& u, int idx, int k) {
+  auto one = [&](const uint4& u, int pp, int k) {
     float f[VEC];
     Vec16<T>::unpack(u, f);
 #pragma unroll
@@ -349,22 +355,29 @@ __global__ __launch_bounds__(256) void gn_fa_kernel(const double2* __restrict__ 
       const float2 q = sab[k * VEC + e];
       f[e] = gn_act(f[e], q.x, q.y, silu);
     }
-    const int p = plo + idx / nch;
-    *(uint4*)(out + ((long)n * HW + p) * C + c0 + k * VEC) = Vec16<T>::pack(f);
+    *(uint4*)(out + ((long)n * HW + plo + pp) * C + c0 + k * VEC) = Vec16<T>::pack(f);
   };
-  int idx = t;
+  int idx = t, pp = t / nch, k = t - (t / nch) * nch;
   for (; idx + 3 * 256 < tot; idx += 4 * 256) {   // four 16-byte loads in flight per thread
-    int k0, k1, k2, k3;
-    const uint4 u0 = *(const uint4*)src_of(idx, k0);
-    const uint4 u1 = *(const uint4*)src_of(idx + 256, k1);
-    const uint4 u2 = *(const uint4*)src_of(idx + 512, k2);
-    const uint4 u3 = *(const uint4*)src_of(idx + 768, k3);
-    one(u0, idx, k0); one(u1, idx + 256, k1); one(u2, idx + 512, k2); one(u3, idx + 768, k3);
+    int p1 = pp, k1 = k;
+    adv(p1, k1);
+    int p2 = p1, k2 = k1;
+    adv(p2, k2);
+    int p3 = p2, k3 = k2;
+    adv(p3, k3);
+    const uint4 u0 = *(const uint4*)src_at(pp, k);
+    const uint4 u1 = *(const uint4*)src_at(p1, k1);
+    const uint4 u2 = *(const uint4*)src_at(p2, k2);
+    const uint4 u3 = *(const uint4*)src_at(p3, k3);
+    one(u0, pp, k); one(u1, p1, k1); one(u2, p2, k2); one(u3, p3, k3);
+    pp = p3;
+    k = k3;
+    adv(pp, k);
   }
   for (; idx < tot; idx += 256) {
-    int k;
-    const uint4 u = *(const uint4*)src_of(idx, k);
-    one(u, idx, k);
+    const uint4 u = *(const uint4*)src_at(pp, k);
+    one(u, pp, k);
+    adv(pp, k);
   }
 }
 
