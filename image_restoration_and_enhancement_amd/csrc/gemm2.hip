@@ -132,11 +132,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
   // HALO == 6 / 7: the per-parity 2x2 convs of a nearest-2x upsampler (GemmArgs::up2_*) on row / strip halo tiles:
   // 4 taps per slab, (ky, kx) = (1 - pad_t + i, 1 - pad_l + j) of the 3x3 halo neighbourhood
   constexpr bool STRIP = HALO == 5 || HALO == 7;
-  constexpr int NTAP = (HALO == 6 || HALO == 7) ? 4 : 9;
+  constexpr int NTAP = (HALO == 6 || HALO == 7 || HALO == 9) ? 4 : 9;
   // HALO == 8: 8 x 8 images (the UNet's 8x8 level), four whole images per 256-row tile: image j's halo is its own
   // 10 x 8 block at halo pixel 80 j (zero rows above / below, never DMA'd), so a tap of tile row r reads halo pixel
   // r + 16 j + 8 ky + kx - 1; K splits finish in the separate reduce kernels (host)
-  constexpr bool MI = HALO == 8;
+  constexpr bool MI = HALO == 8 || HALO == 9;   // (9: the upsampler parity convs of 8x8 images, 4 taps)
   constexpr int HB_U4 = (BM + 2 * kHaloWMax) * CPR;   // one halo slab buffer (uint4)
   constexpr int RING = HALO ? 2 * HB_U4 + S * BN * CPR + CPR + 64 : S * STAGE;
   // (+ a scratch KiB for the surplus DMA pieces, inside the epilogue's staging area when the ring is smaller)
@@ -1792,7 +1792,7 @@ int gemm_emits_gn_parts(const GemmArgs& a) {
   if (a.geglu || a.hs_L || a.batch != 1 || a.out_f32) return 0;
   if (halo_bn(a)) {
     if (halo_mode(a) == 3)   // (8x8 images, K splits reduced by splitk_reduce_gn_kernel: one partial per image)
-      return (g_gn_red_parts && halo_split_count(a, 160) > 1 && a.M % kRedGnRows == 0 && a.N % 64 == 0 && a.act == ACT_NONE && !a.b_rows) ? kRedGnRows
+      return (g_gn_red_parts && !a.up2_w && halo_split_count(a, 160) > 1 && a.M % kRedGnRows == 0 && a.N % 64 == 0 && a.act == ACT_NONE && !a.b_rows) ? kRedGnRows
                                                                                                             : 0;
     return a.M % 256 == 0 ? 256 : 0;
   }
@@ -1989,9 +1989,8 @@ int halo_mode(const GemmArgs& a) {
   const ConvGeom& g = a.g;
   if (!g_conv_halo || !a.conv || a.batch != 1 || a.geglu || a.out_f32 || !vec_ok(a)) return 0;
   if (g.stride != 1) return 0;
-  if (a.up2_w) {   // (ping-pong loop only; whole 256-row tiles of one image: the sub-pixel GroupNorm partial blocks)
+  if (a.up2_w) {   // (ping-pong loop only)
     if (!g_halo_up2 || !g_halo_pipe || a.gn_ab || g.KH != 2 || g.KW != 2 || (g.pad_t & ~1) || (g.pad_l & ~1)) return 0;
-    if (((long)a.up2_h * a.up2_w) % 256) return 0;
   } else if (g.KH != 3 || g.KW != 3 || g.pad_t != 1 || g.pad_l != 1) {
     return 0;
   }
@@ -2001,7 +2000,9 @@ int halo_mode(const GemmArgs& a) {
   if ((long)g.N * g.Hin * W != a.M) return 0;
   // 3 = four whole 8x8 images per tile (HALO == 8): any image count (a partial last tile), so the choice is
   // batch-invariant like the others
-  if (W == 8 && g.Hin == 8 && !a.up2_w && g_halo_mi && g_halo_pipe && !a.gn_ab && a.M % 64 == 0) return 3;
+  if (W == 8 && g.Hin == 8 && g_halo_mi && g_halo_pipe && !a.gn_ab && a.M % 64 == 0) return 3;
+  // (parity convs on row / strip tiles: whole 256-row tiles of one image, the sub-pixel GroupNorm partial blocks)
+  if (a.up2_w && ((long)a.up2_h * a.up2_w) % 256) return 0;
   if (a.M % 256) return 0;
   const bool rows = W >= 16 && W <= kHaloWMax && !(W & (W - 1)) && 256 % W == 0 && g.Hin % (256 / W) == 0;
   // (strips: the ping-pong loop only, no GroupNorm-fused operand)
@@ -2069,8 +2070,9 @@ bool gemm_large_tile(const GemmArgs& a, hipStream_t s) {
     if (g_halo_pipe && !a.gn_ab && b.dbg && a.dtype == BF16) launch2<256, 160, 4, 2, 64, 3, 4>(b, sp, s);   // (diagnostics)
     else
 #endif
-    if (mi) {                           // four 8x8 images per tile
-      launch2<256, 160, 4, 2, 64, 3, 8>(b, sp, s);
+    if (mi) {                           // four 8x8 images per tile (parity convs: 4 taps)
+      if (a.up2_w) launch2<256, 160, 4, 2, 64, 3, 9>(b, sp, s);
+      else launch2<256, 160, 4, 2, 64, 3, 8>(b, sp, s);
     } else if (a.up2_w) {               // upsampler parity convs: 4 taps per slab
       if (halo_mode(a) == 2) launch2<256, 128, 4, 2, 64, 3, 7>(b, sp, s);
       else if (hbn == 160) launch2<256, 160, 4, 2, 64, 3, 6>(b, sp, s);
