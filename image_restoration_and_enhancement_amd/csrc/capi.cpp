@@ -97,6 +97,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"halo_up2", &g_halo_up2, nullptr},
     {"halo_mi", &g_halo_mi, nullptr},
     {"gemm_group", &g_gemm_group, nullptr},
+    {"small_splitk", &g_small_splitk, nullptr},
     {"gemm_pp_chain", &g_gemm_pp_chain, nullptr},
     {"prof_shapes", &g_prof_shapes, nullptr},
     {"attn_prio", &g_attn_prio, nullptr},

@@ -266,6 +266,22 @@ void launch_t(const GemmArgs& a, hipStream_t s) {
 }  // namespace
 
 bool g_large_tiles = true;   // irx_set_option("large_tiles", 0) forces the 4-wave kernel (A/B tests)
+int g_small_splitk = 1;
+
+// K splits for a small-M GEMM on the 4-wave kernel (the CLIP text model's 154 rows, the time embedding's 2B rows): a
+// few 64-column tiles over a long K leave most CUs idle (the CLIP fc2 [154 x 768 x 3072]: 36 blocks, 50 us).  The
+// splits depend on N and K only (every M <= 256 takes the same ones: batch-invariant), whole 64-deep K steps each.
+static int small_splits(const GemmArgs& a) {
+  if (!g_small_splitk || !is16(a.dtype) || a.conv || a.hs_L || a.batch != 1 || a.geglu || a.A1 || a.up2_w) return 0;
+  if (a.M > 256 || a.N % 8 || a.K < 1024 || a.N <= 16) return 0;
+  if (a.out_f32 ? a.ldc % 4 != 0 : (a.ldc % 8 != 0 || ((uintptr_t)a.C % 16) != 0)) return 0;
+  if (a.residual && (a.ldr % 8 != 0 || ((uintptr_t)a.residual % 16) != 0)) return 0;
+  const long ctiles = (a.N + 63) / 64;
+  if (ctiles >= 128) return 0;
+  int sp = 1;
+  while (sp < 8 && ctiles * sp * 2 <= 256 && a.K % (sp * 2 * 64) == 0 && a.K / (sp * 2) >= 256) sp *= 2;
+  return sp > 1 ? sp : 0;
+}
 
 void gemm(const GemmArgs& a, hipStream_t s) {
   const int vec = a.dtype == F32 ? 4 : 8;
@@ -316,6 +332,27 @@ void gemm(const GemmArgs& a, hipStream_t s) {
   // the 4-wave kernel maps rows through c_off for head-split outputs only: a sub-pixel (up2) output would land at
   // low-resolution offsets (gemm_up2_ok does not mirror every early exit of gemm_large_tile)
   IRX_CHECK(!a.up2_w, "a per-parity upsampler conv (up2) needs the large-tile path");
+  if (const int sp = small_splits(a)) {   // raw fp32 partials per K split (the batch index), then the reduce kernel
+    GemmArgs p = a;
+    p.K = a.K / sp;
+    p.batch = sp;
+    p.sA = p.K;
+    p.sB = p.K;
+    p.C = splitk_scratch((size_t)sp * a.M * a.N * sizeof(float));
+    p.ldc = a.N;
+    p.sC = (long)a.M * a.N;
+    p.out_f32 = 1;
+    p.bias = nullptr;
+    p.rowadd = nullptr;
+    p.residual = nullptr;
+    p.act = ACT_NONE;
+    p.alpha = 1.f;
+    p.out_scale = 1.f;
+    if (a.dtype == F16) launch_t<f16_t>(p, s);
+    else launch_t<bf16_t>(p, s);
+    splitk_reduce(a, (const float*)p.C, sp, a.M, a.N, s);
+    return;
+  }
   if (a.dtype == F32) launch_t<float>(a, s);
   else if (a.dtype == F16) launch_t<f16_t>(a, s);
   else launch_t<bf16_t>(a, s);

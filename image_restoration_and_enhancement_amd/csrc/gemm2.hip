@@ -1818,6 +1818,29 @@ bool gemm_up2_ok(const GemmArgs& a) {
          (halo_bn(a) || (!gemm_sk_eligible(a) && choose(a).BM != 0));
 }
 
+// Split-K partials of the 4-wave kernel (gemm.hip, small-M GEMMs) reduced with the large-tile path's kernel: the
+// same fp32 sums over the splits in order, then alpha / bias / row add / activation / residual / output scale
+float* splitk_scratch(size_t bytes) { return internal_ws(bytes); }
+
+void splitk_reduce(const GemmArgs& a, const float* ws, int splits, int Mp, int Np, hipStream_t s) {
+  IRX_CHECK(a.N % 8 == 0 && a.batch == 1 && is16(a.dtype), "splitk_reduce: 16-bit, N % 8 == 0, batch 1");
+  const char* tn = a.dtype == F16 ? "_Float16" : "unsigned short";
+  ProfScope ps(prof_on() ? std::string("irx::(anonymous namespace)::splitk_reduce_kernel<") + tn + ", " +
+                               (a.out_f32 ? "true" : "false") + ">"
+                         : std::string(),
+               0.0, s);
+  const long n = (long)a.M * (a.N / 8);
+  const dim3 g2((unsigned)((n + 255) / 256), 1);
+  if (a.dtype == F16) {
+    if (a.out_f32) splitk_reduce_kernel<f16_t, true><<<g2, 256, 0, s>>>(a, ws, splits, Mp, Np);
+    else splitk_reduce_kernel<f16_t, false><<<g2, 256, 0, s>>>(a, ws, splits, Mp, Np);
+  } else {
+    if (a.out_f32) splitk_reduce_kernel<bf16_t, true><<<g2, 256, 0, s>>>(a, ws, splits, Mp, Np);
+    else splitk_reduce_kernel<bf16_t, false><<<g2, 256, 0, s>>>(a, ws, splits, Mp, Np);
+  }
+  IRX_LAUNCH_CHECK();
+}
+
 int g_gemm_pp_chain = 1;   // irx_set_option("gemm_pp_chain", 0): the two-source 1x1 chains on the two-stage loop (A/B)
 
 int g_ln_fold = 1;

@@ -144,6 +144,9 @@ __host__ __device__ __forceinline__ long c_off_f(long m, int n, long ldc, int M,
 bool gemm_up2_ok(const GemmArgs& a);   // the large-tile path can store a sub-pixel (GemmArgs::up2_*) output
 void gemm(const GemmArgs& a, hipStream_t s);
 bool gemm_large_tile(const GemmArgs& a, hipStream_t s);   // 8-wave LDS-DMA path; false if not eligible
+float* splitk_scratch(size_t bytes);                     // the library's split-K partial scratch (grown on demand)
+void splitk_reduce(const GemmArgs& a, const float* ws, int splits, int Mp, int Np, hipStream_t s);
+extern int g_small_splitk;   // 1 (default): small-M, long-K 4-wave GEMMs in K splits + the reduce kernel
 // A 1x1 / stride-1 / unpadded conv (optionally over a channel concat) rewritten as a dense GEMM over the NHWC
 // rows (A = src0, A1 = src1 from K = C0) when the large-tile path takes it (option conv1x1_dense): the
 // im2col walk's per-tap machinery buys nothing at one tap.  Returns whether `a` was rewritten.

@@ -898,3 +898,34 @@ def test_conv_halo_8x8_images(device, case, dt):
     assert O.rel_err(got, walk.float()) < (8e-3 if dt == torch.bfloat16 else 2e-3)
     err = (got.float().cpu() - ref).abs().amax(dim=-1)   # every pixel: image seams and pad rows
     assert float(err.max()) < 0.05 * float(ref.abs().max()), err.argmax()
+
+
+@pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("M,N,K,act,res", [
+    (154, 768, 3072, 0, True),    # CLIP fc2 (+ residual): 8 K splits
+    (16, 1280, 1280, 1, False),   # time embedding linear_2 (+ SiLU): 4 K splits
+    (154, 768, 768, 0, True),     # K < 1024: no split (the plain 4-wave kernel)
+])
+def test_small_m_splitk(device, dt, M, N, K, act, res):
+    """Small-M, long-K GEMMs on the 4-wave kernel in K splits + the split-K reduce kernel (option small_splitk):
+    vs PyTorch fp32 on the same rounded operands, vs the unsplit kernel within fp32 reassociation, and batch-invariant
+    (the split depends on N and K only: the first rows of an M-row call equal a 6-row call bit for bit)."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    A = _r(M, K, seed=700)
+    Bw = _r(N, K, seed=701, scale=1 / math.sqrt(K))
+    bias, R = _r(N, seed=702), _r(M, N, seed=703)
+    dA, dB = _dev(A, dt, device), _dev(Bw, dt, device)
+    dR = _dev(R, dt, device) if res else None
+    got = O.gemm(dA, dB, bias=bias.to(device), act=act, residual=dR)
+    with L.option(small_splitk=0):
+        plain = O.gemm(dA, dB, bias=bias.to(device), act=act, residual=dR)
+    six = O.gemm(dA[:6].contiguous(), dB, bias=bias.to(device), act=act, residual=dR[:6].contiguous() if res else None)
+    torch.cuda.synchronize()
+    ref = _q(A, dt) @ _q(Bw, dt).T + bias
+    if act == 1:
+        ref = F.silu(ref)
+    if res:
+        ref = ref + _q(R, dt)
+    assert O.rel_err(got, ref) < TOL[dt]
+    assert O.rel_err(got, plain.float()) < (8e-3 if dt == torch.bfloat16 else 2e-3)
+    assert torch.equal(got[:6], six)
