@@ -270,9 +270,10 @@ int g_small_splitk = 1;
 
 // K splits for a small-M GEMM on the 4-wave kernel (the CLIP text model's 154 rows, the time embedding's 2B rows): a
 // few 64-column tiles over a long K leave most CUs idle (the CLIP fc2 [154 x 768 x 3072]: 36 blocks, 50 us).  The
-// splits depend on N and K only (every M <= 256 takes the same ones: batch-invariant), whole 64-deep K steps each.
+// splits depend on N and K only (every M <= 256 takes the same ones: batch-invariant), whole 64-deep K steps each,
+// and not on the output layout (a head-split q|k|v projection takes the same splits as its row-major twin).
 static int small_splits(const GemmArgs& a) {
-  if (!g_small_splitk || !is16(a.dtype) || a.conv || a.hs_L || a.batch != 1 || a.geglu || a.A1 || a.up2_w) return 0;
+  if (!g_small_splitk || !is16(a.dtype) || a.conv || a.batch != 1 || a.geglu || a.A1 || a.up2_w) return 0;
   if (a.M > 256 || a.N % 8 || a.K < 1024 || a.N <= 16) return 0;
   if (a.out_f32 ? a.ldc % 4 != 0 : (a.ldc % 8 != 0 || ((uintptr_t)a.C % 16) != 0)) return 0;
   if (a.residual && (a.ldr % 8 != 0 || ((uintptr_t)a.residual % 16) != 0)) return 0;
@@ -339,6 +340,7 @@ void gemm(const GemmArgs& a, hipStream_t s) {
     p.sA = p.K;
     p.sB = p.K;
     p.C = splitk_scratch((size_t)sp * a.M * a.N * sizeof(float));
+    p.hs_L = 0;           // partials row-major; the reduce kernel maps head-split rows (c_off)
     p.ldc = a.N;
     p.sC = (long)a.M * a.N;
     p.out_f32 = 1;

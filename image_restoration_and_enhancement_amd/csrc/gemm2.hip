@@ -1094,7 +1094,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
       // (halo conv tiles only: the GroupNorm-partial loop of the 256x320 tiles spilled with it; on the 128x320
       //  tiles of proj_out ∘ ff.net.2 at 32^2 / 16^2 it measured no faster, profiles/r05_bench_shapes_chain.txt)
       constexpr bool kEpiPrefetch = HALO != 0;
-      constexpr int kEpiPF = 4;
+      constexpr int kEpiPF = BN <= 128 ? 8 : 6;   // rows per residual batch (256x128: a thread's 8 rows, 256x160: 11 in 2)
       // chunk swizzle inside whole groups of 8 chunks only (BN = 160 leaves a 4-chunk tail unswizzled)
       auto csw = [](int c, int row) { return c < (CPR & ~7) ? c ^ (row & 7) : c; };
       if (a.ln_rs || a.ln_part) {
