@@ -177,6 +177,46 @@ def pmc_counters(kernel: str) -> dict:
     return {}
 
 
+def bucket(name: str) -> str:
+    """Kernel family of a profiled launch: the step's time buckets."""
+    n = _norm_kernel(name)
+    if n.startswith("irx::gemm2_kernel<") or n.startswith("_ZN3irx12_GLOBAL__N_112gemm2_kernel"):
+        args = n[n.index("<") + 1:].split(",") if "<" in n else []
+        return "conv" if (len(args) > 7 and args[7] == "true") or "Lb1ELb0ELb0ELi" in n else "dense"
+    if "gn_conv_narrow" in n:
+        return "conv"
+    if "gemm" in n or "splitk_reduce" in n:
+        return "dense"
+    if "attn" in n:
+        return "attention"
+    if n.startswith("irx::gn_") or n.startswith("irx::ln_") or "norm" in n:
+        return "norm"
+    return "other"
+
+
+def bucket_summary(prof: list, steps: int) -> dict:
+    """Per kernel family: ms/step, algorithmic TF/s, and HBM GB/s against the 8 TB/s peak over the launches whose
+    HBM bytes a committed PMC pass holds (pmc_counters; `hbm_covered_ms` says how much of the bucket that is)."""
+    out = {}
+    for name, cnt, ms, fl in prof:
+        b = out.setdefault(bucket(name), {"ms": 0.0, "fl": 0.0, "pmc_ms": 0.0, "bytes": 0.0})
+        b["ms"] += ms
+        b["fl"] += fl
+        t = pmc_counters(name).get("traffic")
+        if t:
+            b["pmc_ms"] += ms
+            b["bytes"] += float(t) * cnt
+    res = {}
+    for k, b in sorted(out.items(), key=lambda kv: -kv[1]["ms"]):
+        gbps = b["bytes"] / (b["pmc_ms"] * 1e-3) / 1e9 if b["pmc_ms"] else None
+        res[k] = {"ms_per_step": round(b["ms"] / steps, 2),
+                  "tflops": round(b["fl"] / (b["ms"] * 1e-3) / 1e12, 1) if b["ms"] and b["fl"] else None,
+                  "hbm_gbps": round(gbps, 1) if gbps else None,
+                  "hbm_frac": round(gbps / 8000.0, 4) if gbps else None,
+                  "hbm_covered_ms_per_step": round(b["pmc_ms"] / steps, 2)}
+    return res
+
+
 def usable_cpus() -> int:
     """CPUs this process may run on: sched affinity, capped by a cgroup CPU quota when one is set."""
     n = len(os.sched_getaffinity(0))
@@ -404,7 +444,8 @@ def main():
                     "launches": cnt, "avg_launch_us": round(ms * 1e3 / cnt, 2),
                     "flops_per_launch": fl / cnt,
                     "all_mfma_kernels_tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 2),
-                    "mfma_kernel_ms_per_step": round(tot_ms / args.steps, 2)}
+                    "mfma_kernel_ms_per_step": round(tot_ms / args.steps, 2),
+                    "buckets": bucket_summary(prof, args.steps)}
 
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -1049,7 +1049,8 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
                            std::to_string(KT) + ">"
                      : "irx::(anonymous namespace)::attn3_kernel<" + tn + ", " + std::to_string(D) + ", " +
                            std::to_string(KT) + ", " + (CAUSAL ? "true" : "false") + ", " +
-                           (kind == kRes ? "true" : "false") + ", " + (kind == kPf ? "3" : "0") + ">";
+                           (kind == kRes ? "true" : "false") + ", " +
+                           (kind == kPf ? "3" : (D == 160 && g_attn_pf160 && kind != kQ2) ? "1" : "0") + ">";
     if (g_prof_shapes)
       nm += " [B " + std::to_string(a.B) + " Lq " + std::to_string(a.Lq) + " Lk " + std::to_string(a.Lk) + "]";
   }
@@ -1059,6 +1060,14 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
   b.prio = g_attn_prio;
   b.qrep = qrep;
   if constexpr (!CAUSAL) {
+    if constexpr (D == 160) {   // one wave per SIMD: the whole-tile fragment prefetch in the register file's other half
+      if (g_attn_pf160 && kind != kQ2) {
+        if (kind == kRes) attn3_kernel<T, D, KT, false, true, 1><<<grid, block, 0, s>>>(b);
+        else attn3_kernel<T, D, KT, false, false, 1><<<grid, block, 0, s>>>(b);
+        IRX_LAUNCH_CHECK();
+        return;
+      }
+    }
     if (kind == kRes) {
       attn3_kernel<T, D, KT, false, true><<<grid, block, 0, s>>>(b);
       IRX_LAUNCH_CHECK();
@@ -1142,7 +1151,8 @@ void attention(const AttnArgs& a, hipStream_t s) {
   }
 }
 int g_attn_q2 = 1;     // irx_set_option("attn_q2", 0): d = 40 self-attention with one query group per wave (attn3, A/B)
-int g_attn_pf = 1;     // irx_set_option("attn_pf", 0): d = 40 self-attention without the whole-tile fragment prefetch (A/B)
+int g_attn_pf = 1;
+int g_attn_pf160 = 1;   // irx_set_option("attn_pf160", 0): d = 160 without the fragment prefetch (A/B)     // irx_set_option("attn_pf", 0): d = 40 self-attention without the whole-tile fragment prefetch (A/B)
 int g_attn_xcd = 1;
 int g_attn_prio = 0;
 int g_attn_qrep = 1;   // irx_set_option("attn_qrep", 0): one query group per block in cross-attention (A/B); >= 2: that many (sweeps)   // irx_set_option("attn_prio", 1): MFMA chains of attn3 at raised wave priority (A/B)

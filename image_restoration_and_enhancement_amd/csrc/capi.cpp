@@ -78,6 +78,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gn_fold", &g_gn_fold, nullptr},
     {"gn_narrow", &g_gn_narrow, nullptr},
     {"attn_pf", &g_attn_pf, nullptr},
+    {"attn_pf160", &g_attn_pf160, nullptr},
     {"attn_q2", &g_attn_q2, nullptr},
     {"conv1x1_dense", &g_conv1x1_dense, nullptr},
     {"gn_fa", &g_gn_fa, nullptr},

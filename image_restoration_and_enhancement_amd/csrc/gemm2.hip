@@ -244,8 +244,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
     retarget();
   }
 
+  // (LDS byte addresses from one cast of the array base: a per-piece generic -> LDS pointer cast can leave a null
+  //  test on the shared aperture that the diagnostic builds' early exits fail to fold)
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)smem);
   auto issue = [&](int kt, int stage) {
-    uint4* sbase = smem + stage * STAGE;
     int koffA = CONV ? (kc >= a.g.C0 ? kc - a.g.C0 : kc) : kt * BK;
     if constexpr (!CONV) {
       if (A1p && koffA >= a.kA1) {      // the concat's second source (steps are issued in order: one switch)
@@ -261,8 +263,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void gemm2_kern
 #pragma unroll
     for (int j = 0; j < IPW; ++j) {
       const uint16_t* src = rb[j] ? rb[j] + ((isA[j] ? koffA : koffB) + lk[j]) : zp;
-      uint4* dst = live[j] ? sbase + (wave * IPW + j) * 64 : smem + SMEM - 64;
-      glds16_asm(src, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)dst));
+      const uint32_t dst = live[j] ? lds_base + (uint32_t)(stage * STAGE + (wave * IPW + j) * 64) * 16u
+                                   : lds_base + (uint32_t)(SMEM - 64) * 16u;
+      glds16_asm(src, __builtin_amdgcn_readfirstlane(dst));
     }
     if constexpr (CONV) {
       kc += BK;

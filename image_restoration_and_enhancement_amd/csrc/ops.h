@@ -259,6 +259,7 @@ struct AttnArgs {
 void attention(const AttnArgs& a, hipStream_t s);
 extern int g_attn_q2;    // 1: non-causal streamed d = 40 attention with two 32-query groups per wave (attn3q)
 extern int g_attn_pf;    // 1: non-causal streamed d = 40 attention with whole-tile K / V fragment prefetch (attn3 PF)
+extern int g_attn_pf160;   // 1: d = 160 attention (streamed and resident K/V) with the whole-tile fragment prefetch
 extern int g_attn_prio;
 extern int g_attn_qrep;
 extern int g_attn_xcd;   // 1: (batch, head) groups of q-blocks kept on one XCD (K/V shared in its L2)

@@ -166,6 +166,8 @@ def main():
             flops = 4.0 * B * Lq * Lk * C
             res = []
             avs = (("pf", {"attn_pf": 1, "attn_q2": 0}), ("q2", {"attn_pf": 1, "attn_q2": 1}))
+            if C // 8 == 160:   # d = 160: with / without the whole-tile fragment prefetch
+                avs = (("pf160", {"attn_pf160": 1}), ("nopf", {"attn_pf160": 0}))
             if args.attn_qrep and Lk <= 128:   # resident-K/V query groups per block: auto vs forced counts
                 avs = (("auto", {"attn_qrep": 1}),) + tuple((f"qr{q}", {"attn_qrep": q}) for q in (2, 4, 8, 16)) + \
                       (("auto", {"attn_qrep": 1}),)

@@ -707,6 +707,25 @@ def test_attention_prefetch_d40_bit_exact(device, dt, B, Lq, Lk):
 
 
 @pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("B,Lq,Lk", [(2, 256, 256), (1, 64, 64), (2, 256, 77), (1, 64, 77), (1, 333, 190), (1, 100, 128)])
+def test_attention_prefetch_d160_bit_exact(device, dt, B, Lq, Lk):
+    """d = 160 (the UNet's 16x16 / 8x8 levels, one wave per SIMD) with the whole-tile fragment prefetch (option
+    attn_pf160), streamed (Lk > 128) and resident K/V (Lk <= 128, the 77 text tokens): the same MFMAs on the same
+    operands in the same order as without it — identical bit for bit."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    C, heads = 1280, 8
+    q, k, v = _r(B, Lq, C, seed=79) * 2, _r(B, Lk, C, seed=80) * 2, _r(B, Lk, C, seed=81)
+    qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
+    with L.option(attn_pf160=1):
+        got = O.attention(qd, kd, vd, heads)
+    with L.option(attn_pf160=0):
+        base = O.attention(qd, kd, vd, heads)
+    torch.cuda.synchronize()
+    assert torch.equal(got, base)
+    assert O.rel_err(got, O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), heads, False)) < TOL[dt] * 2
+
+
+@pytest.mark.parametrize("dt", DT16)
 @pytest.mark.parametrize("B,Lq,Lk", [(2, 1024, 1024), (1, 333, 190), (1, 64, 129), (2, 4096, 4096)])
 def test_attention_two_query_groups_d40_bit_exact(device, dt, B, Lq, Lk):
     """attn3q (option attn_q2: two 32-query groups per wave sharing every K / V^T fragment read) runs each group's
