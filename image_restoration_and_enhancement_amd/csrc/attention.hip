@@ -13,6 +13,7 @@
 #include "profile.h"
 
 namespace irx {
+extern int g_attn_pf80;
 namespace {
 
 constexpr int kWaves = 4;
@@ -354,8 +355,21 @@ __global__ __launch_bounds__(256, (PF ? PF : attn3_occ<D, KT>())) void attn3_ker
   const T* __restrict__ V = (const T*)a.v + (long)b * a.sv + (long)h * (a.hsv ? a.hsv : D);
 
   // pad columns: K[.][d] = 1 when -m rides in the padding (PADM below), V[.][d] = 1 for the row sums
-  for (int i = tid; i < 2 * KT * SK; i += 256) Ks2[i] = (DQ > D && i % SK == D) ? one_bits<T>() : (uint16_t)0;
-  for (int i = tid; i < 2 * KT * SV; i += 256) Vs2[i] = (ONES && i % SV == D) ? one_bits<T>() : (uint16_t)0;
+  // (16-byte chunks: SK, SV and D are multiples of 8, so column d is element 0 of its chunk)
+  static_assert(SK % 8 == 0 && SV % 8 == 0, "pad-column chunks");
+  // (the pad element selected as a scalar: a select between two uint4 constants becomes a scratch-memory table).
+  // d = 160: 164 two-byte stores per thread became 21 (self-attention L = 256 21.6 -> 17.5 us); the streamed d = 80
+  // kernel keeps the element loop (its main loop scheduled 4 % slower with the chunked one, profiles/r06_kbench_attn_init.txt)
+  constexpr bool VINIT = RES || D != 80;
+  if constexpr (VINIT) {
+    for (int i = tid; i < 2 * KT * SK / 8; i += 256)
+      ((uint4*)Ks2)[i] = make_uint4((DQ > D && (8 * i) % SK == D) ? (unsigned)one_bits<T>() : 0u, 0u, 0u, 0u);
+    for (int i = tid; i < 2 * KT * SV / 8; i += 256)
+      ((uint4*)Vs2)[i] = make_uint4((ONES && (8 * i) % SV == D) ? (unsigned)one_bits<T>() : 0u, 0u, 0u, 0u);
+  } else {
+    for (int i = tid; i < 2 * KT * SK; i += 256) Ks2[i] = (DQ > D && i % SK == D) ? one_bits<T>() : (uint16_t)0;
+    for (int i = tid; i < 2 * KT * SV; i += 256) Vs2[i] = (ONES && i % SV == D) ? one_bits<T>() : (uint16_t)0;
+  }
 
   // per-thread staging slots (row, 16-byte chunk) of a K/V tile, fixed for the kernel: pointers and LDS offsets
   // computed once; a full tile (every row < Lk) loads with no per-row checks
@@ -374,6 +388,33 @@ __global__ __launch_bounds__(256, (PF ? PF : attn3_occ<D, KT>())) void attn3_ker
     vsoff[u] = row * SV + c * 8;
   }
   auto slot_ok = [&](int u) { return u < NCH - 1 || tid + 256 * u < KT * CPR; };
+  auto load_to = [&](int j0, uint4 (&kr)[NCH], uint4 (&vr)[NCH]) {
+    const long ko = (long)j0 * a.ldk, vo = (long)j0 * a.ldv;
+    if (j0 + KT <= a.Lk) {
+#pragma unroll
+      for (int u = 0; u < NCH; ++u)
+        if (slot_ok(u)) {
+          kr[u] = *(const uint4*)(kp[u] + ko);
+          vr[u] = *(const uint4*)(vp[u] + vo);
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const bool in = j0 + krow[u] < a.Lk;
+        kr[u] = in ? *(const uint4*)(kp[u] + ko) : make_uint4(0, 0, 0, 0);
+        vr[u] = in ? *(const uint4*)(vp[u] + vo) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto stage_from = [&](int buf, const uint4 (&kr)[NCH], const uint4 (&vr)[NCH]) {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u)
+      if (slot_ok(u)) {
+        *(uint4*)(Ks2 + buf * KT * SK + ksoff[u]) = kr[u];
+        *(uint4*)(Vs2 + buf * KT * SV + vsoff[u]) = vr[u];
+      }
+  };
+  // (the streamed loop's own copies: routed through load_to / stage_from, the d = 80 kernel's loop scheduled worse)
   auto load = [&](int j0) {
     const long ko = (long)j0 * a.ldk, vo = (long)j0 * a.ldv;
     if (j0 + KT <= a.Lk) {
@@ -400,28 +441,53 @@ __global__ __launch_bounds__(256, (PF ? PF : attn3_occ<D, KT>())) void attn3_ker
         *(uint4*)(Vs2 + buf * KT * SV + vsoff[u]) = vreg[u];
       }
   };
+  // raw Q^T fragments of query group rep (B operand): lane (r, hh) holds q[qrow][16s + 8hh .. +7].  RES: the next
+  // group's are requested before the current group's MFMAs (their latency hides under them; QPF, where the register
+  // budget allows), and group 0's together with both K/V tiles — one global round trip before the first MFMA
+  // instead of three (K/V tile 0 -> stage -> tile 1 -> stage -> Q).  Only the order of the loads changes.
+  constexpr bool QPF = RES && D <= 80;
+  uint4 qn[NS];
+  auto loadq = [&](int rep) {
+    const int qr = (qb * qrep + rep) * QB + wave * 32 + r;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int e = 16 * s + 8 * hh;
+      qn[s] = (qr < a.Lq && e < D) ? *(const uint4*)(Q + (long)qr * a.ldq + e) : make_uint4(0, 0, 0, 0);
+    }
+  };
   if constexpr (RES) {
+    uint4 k1[NCH], v1[NCH];
+    const bool two = KT < a.Lk;
+    loadq(0);
     load(0);
+    if (two) load_to(KT, k1, v1);
     __syncthreads();          // pad-column initialisation complete
     stage(0);
-    if (KT < a.Lk) {
-      load(KT);
-      stage(1);
-    }
+    if (two) stage_from(1, k1, v1);
     __syncthreads();
   }
 
   for (int rep = 0; rep < qrep; ++rep) {
   const int q0 = (qb * qrep + rep) * QB + wave * 32;
   const int qrow = q0 + r;
-  // Q^T fragments (B operand): lane (r, hh) holds q[qrow][16s + 8hh .. +7], pre-scaled by scale*log2(e)
+  // Q^T fragments (B operand), pre-scaled by scale*log2(e)
   uint4 qf[NS];
   const float sl2 = a.scale * 1.4426950408889634f;
+  if constexpr (RES) {
+    if (rep > 0 && !QPF) loadq(rep);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[s] = qn[s];
+    if constexpr (QPF) {
+      if (rep + 1 < qrep) loadq(rep + 1);
+    }
+  }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const int e = 16 * s + 8 * hh;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (qrow < a.Lq && e < D) v = *(const uint4*)(Q + (long)qrow * a.ldq + e);
+    uint4 v = RES ? qf[s] : make_uint4(0, 0, 0, 0);
+    if constexpr (!RES) {   // (streamed K/V: the Q loads in front of the first K/V tile's, as before)
+      const int e = 16 * s + 8 * hh;
+      if (qrow < a.Lq && e < D) v = *(const uint4*)(Q + (long)qrow * a.ldq + e);
+    }
     if (!a.q_scaled) {
       float f[8];
       Vec16<T>::unpack(v, f);
@@ -1050,7 +1116,10 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
                      : "irx::(anonymous namespace)::attn3_kernel<" + tn + ", " + std::to_string(D) + ", " +
                            std::to_string(KT) + ", " + (CAUSAL ? "true" : "false") + ", " +
                            (kind == kRes ? "true" : "false") + ", " +
-                           (kind == kPf ? "3" : (D == 160 && g_attn_pf160 && kind != kQ2) ? "1" : "0") + ">";
+                           (kind == kPf ? "3"
+                            : (D == 160 && g_attn_pf160 && kind != kQ2) ? "1"
+                            : (D == 80 && kind == kPlain && g_attn_pf80 == 2) ? "2"
+                                                                                                    : "0") + ">";
     if (g_prof_shapes)
       nm += " [B " + std::to_string(a.B) + " Lq " + std::to_string(a.Lq) + " Lk " + std::to_string(a.Lk) + "]";
   }
@@ -1064,6 +1133,13 @@ void launch3_cfg(const AttnArgs& a, hipStream_t s) {
       if (g_attn_pf160 && kind != kQ2) {
         if (kind == kRes) attn3_kernel<T, D, KT, false, true, 1><<<grid, block, 0, s>>>(b);
         else attn3_kernel<T, D, KT, false, false, 1><<<grid, block, 0, s>>>(b);
+        IRX_LAUNCH_CHECK();
+        return;
+      }
+    }
+    if constexpr (D == 80) {   // (option attn_pf80 = 2: the whole-tile fragment prefetch at 2 waves per SIMD)
+      if (kind == kPlain && g_attn_pf80 == 2) {
+        attn3_kernel<T, D, KT, false, false, 2><<<grid, block, 0, s>>>(b);   // (PF 3 spills)
         IRX_LAUNCH_CHECK();
         return;
       }
@@ -1150,12 +1226,14 @@ void attention(const AttnArgs& a, hipStream_t s) {
     launch_t<bf16_t>(a, s);
   }
 }
-int g_attn_q2 = 1;     // irx_set_option("attn_q2", 0): d = 40 self-attention with one query group per wave (attn3, A/B)
-int g_attn_pf = 1;
-int g_attn_pf160 = 1;   // irx_set_option("attn_pf160", 0): d = 160 without the fragment prefetch (A/B)     // irx_set_option("attn_pf", 0): d = 40 self-attention without the whole-tile fragment prefetch (A/B)
+int g_attn_q2 = 1;      // irx_set_option("attn_q2", 0): d = 40 self-attention with one query group per wave (attn3, A/B)
+int g_attn_pf = 1;      // irx_set_option("attn_pf", 0): d = 40 self-attention without the whole-tile fragment prefetch (A/B)
+int g_attn_pf160 = 1;   // irx_set_option("attn_pf160", 0): d = 160 without the fragment prefetch (A/B)
+int g_attn_pf80 = 2;    // irx_set_option("attn_pf80", 0): d = 80 self-attention without the whole-tile fragment prefetch
+                        // (A/B; 2 = at 2 waves / SIMD: L = 1024 67.2 -> 61.1 us, profiles/r06_kbench_attn_init.txt)
 int g_attn_xcd = 1;
-int g_attn_prio = 0;
-int g_attn_qrep = 1;   // irx_set_option("attn_qrep", 0): one query group per block in cross-attention (A/B); >= 2: that many (sweeps)   // irx_set_option("attn_prio", 1): MFMA chains of attn3 at raised wave priority (A/B)
+int g_attn_prio = 0;    // irx_set_option("attn_prio", 1): MFMA chains of attn3 at raised wave priority (A/B)
+int g_attn_qrep = 1;    // irx_set_option("attn_qrep", 0): one query group per block in cross-attention (A/B); >= 2: that many (sweeps)
 int g_attn_hm = 1;
 
 }  // namespace irx

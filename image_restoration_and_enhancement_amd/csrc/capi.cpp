@@ -14,6 +14,7 @@ namespace irx {
 static thread_local std::string g_err;
 void set_error(const std::string& m) { g_err = m; }
 const char* last_error() { return g_err.c_str(); }
+extern int g_attn_pf80;   // (attention.hip)
 }  // namespace irx
 
 using namespace irx;
@@ -79,6 +80,7 @@ static const struct { const char* name; int* i; bool* b; } kOpts[] = {
     {"gn_narrow", &g_gn_narrow, nullptr},
     {"attn_pf", &g_attn_pf, nullptr},
     {"attn_pf160", &g_attn_pf160, nullptr},
+    {"attn_pf80", &g_attn_pf80, nullptr},
     {"attn_q2", &g_attn_q2, nullptr},
     {"conv1x1_dense", &g_conv1x1_dense, nullptr},
     {"gn_fa", &g_gn_fa, nullptr},

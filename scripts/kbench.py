@@ -92,6 +92,7 @@ def main():
     ap.add_argument("--ref", action="store_true", help="also time torch (hipBLASLt / MIOpen) on the same shapes")
     ap.add_argument("--variants", default="s2,ring64,small")
     ap.add_argument("--attn-qrep", action="store_true", help="cross-attention: sweep the resident-K/V query groups")
+    ap.add_argument("--pf80", action="store_true", help="d = 80 self-attention: option attn_pf80 on / off")
     args = ap.parse_args()
     dev = torch.device("cuda")
     L.load()
@@ -168,6 +169,8 @@ def main():
             avs = (("pf", {"attn_pf": 1, "attn_q2": 0}), ("q2", {"attn_pf": 1, "attn_q2": 1}))
             if C // 8 == 160:   # d = 160: with / without the whole-tile fragment prefetch
                 avs = (("pf160", {"attn_pf160": 1}), ("nopf", {"attn_pf160": 0}))
+            if args.pf80 and C // 8 == 80 and Lk > 128:   # d = 80 self-attention: with / without the fragment prefetch
+                avs = (("pf80", {"attn_pf80": 2}), ("base", {"attn_pf80": 0}))
             if args.attn_qrep and Lk <= 128:   # resident-K/V query groups per block: auto vs forced counts
                 avs = (("auto", {"attn_qrep": 1}),) + tuple((f"qr{q}", {"attn_qrep": q}) for q in (2, 4, 8, 16)) + \
                       (("auto", {"attn_qrep": 1}),)

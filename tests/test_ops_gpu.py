@@ -726,6 +726,24 @@ def test_attention_prefetch_d160_bit_exact(device, dt, B, Lq, Lk):
 
 
 @pytest.mark.parametrize("dt", DT16)
+@pytest.mark.parametrize("B,Lq,Lk", [(2, 1024, 1024), (1, 333, 190), (1, 64, 129), (2, 130, 300)])
+def test_attention_prefetch_d80_bit_exact(device, dt, B, Lq, Lk):
+    """d = 80 self-attention (the UNet's 32x32 level) with the whole-tile fragment prefetch at 2 waves / SIMD (option
+    attn_pf80, default 2): the same MFMAs on the same operands in the same order as the kernel without it."""
+    from image_restoration_and_enhancement_amd import _lib as L
+    C, heads = 640, 8
+    q, k, v = _r(B, Lq, C, seed=82) * 2, _r(B, Lk, C, seed=83) * 2, _r(B, Lk, C, seed=84)
+    qd, kd, vd = _dev(q, dt, device), _dev(k, dt, device), _dev(v, dt, device)
+    with L.option(attn_pf80=2):
+        got = O.attention(qd, kd, vd, heads)
+    with L.option(attn_pf80=0):
+        base = O.attention(qd, kd, vd, heads)
+    torch.cuda.synchronize()
+    assert torch.equal(got, base)
+    assert O.rel_err(got, O.ref_attention(_q(q, dt), _q(k, dt), _q(v, dt), heads, False)) < TOL[dt] * 2
+
+
+@pytest.mark.parametrize("dt", DT16)
 @pytest.mark.parametrize("B,Lq,Lk", [(2, 1024, 1024), (1, 333, 190), (1, 64, 129), (2, 4096, 4096)])
 def test_attention_two_query_groups_d40_bit_exact(device, dt, B, Lq, Lk):
     """attn3q (option attn_q2: two 32-query groups per wave sharing every K / V^T fragment read) runs each group's
