@@ -2,6 +2,7 @@
 # Same-box A/B of the default bench step: the current library vs a saved baseline (scripts/_ab/libirx_base.so),
 # alternated twice; each line -> gpurun_out/<tag>/{new,base}_<i>.json
 set -u
+export IRX_PROF_TOP=${IRX_PROF_TOP:-80}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${1:-ab_bench}; shift || true
 mkdir -p "$O"

@@ -93,6 +93,7 @@ def main():
     ap.add_argument("--variants", default="s2,ring64,small")
     ap.add_argument("--attn-qrep", action="store_true", help="cross-attention: sweep the resident-K/V query groups")
     ap.add_argument("--pf80", action="store_true", help="d = 80 self-attention: option attn_pf80 on / off")
+    ap.add_argument("--lnout", action="store_true", help="residual-stream producers with / without LayerNorm partials")
     args = ap.parse_args()
     dev = torch.device("cuda")
     L.load()
@@ -139,6 +140,25 @@ def main():
                 ms = timeit(lambda: torch.nn.functional.conv2d(xr, wr, None, s, k // 2), args.iters)
                 res.append(f"miopen {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
             print(f"{lab:24s} " + " | ".join(res), flush=True)
+    if args.lnout:   # the transformer residual-stream producers: + residual, in place, with / without LN partials
+        for M, N, K in ((65536, 320, 320), (16384, 640, 640)):
+            A = torch.randn(M, K, device=dev, generator=g).to(dt)
+            Bw = (torch.randn(N, K, device=dev, generator=g) / math.sqrt(K)).to(dt)
+            bias = torch.zeros(N, device=dev)
+            R = torch.randn(M, N, device=dev, generator=g).to(dt)
+            C = R.clone()
+            parts = torch.empty(M, max(1, N // 320), 2, device=dev)
+            flops = 2.0 * M * N * K
+            setv({})
+            res = []
+            runs = [("res", lambda: O.gemm(A, Bw, bias=bias, residual=R)),
+                    ("inplace", lambda: O.gemm(A, Bw, bias=bias, residual=C)),
+                    ("lnout", lambda: L.call("irx_op_gemm_ln_out", O.S(), O.DT[dt], M, N, K, O.P(A), O.P(Bw), O.P(bias),
+                                             O.P(C), O.P(C), O.P(parts), 1 if N == 320 else 0, 1e-5))]
+            for vn, fn in runs:
+                ms = timeit(fn, args.iters)
+                res.append(f"{vn} {ms * 1e3:8.1f}us {flops / ms / 1e9:7.1f}TF")
+            print(f"lnout M{M} N{N} K{K}      " + " | ".join(res), flush=True)
     if args.only in ("", "gemm"):
         for lab, M, N, K, *extra in GEMMS:
             if args.match not in lab:
