@@ -1093,12 +1093,15 @@ void launchw(const AttnArgs& a, hipStream_t s) {
 
 template <typename T, int D, int KT, bool CAUSAL>
 void launch3_cfg(const AttnArgs& a, hipStream_t s) {
-  // query groups per block against resident K/V (cross-attention, Lk <= 2 KT): as many as keep >= 1024 blocks
+  // query groups per block against resident K/V (cross-attention, Lk <= 2 KT): as many as keep >= 1024 blocks at
+  // d = 40 (4 blocks / CU resident), >= 512 at the wider heads (kbench sweep with the one-round-trip prologue,
+  // profiles/r06_kbench_attn_qrep.txt: d = 80 19.8 -> 17.0 us at 2 groups; d = 40 best at 4, d = 160 at 1)
   const bool res = !CAUSAL && a.Lk <= 2 * KT && g_attn_qrep;
+  const long min_blocks = D <= 40 ? 1024 : 512;
   int qrep = 1;
   if (res && g_attn_qrep >= 2) qrep = std::min(g_attn_qrep, 32);   // (sweeps: a forced count)
   else if (res)
-    while (qrep < 8 && ((a.Lq + 128 * 2 * qrep - 1) / (128 * 2 * qrep)) * a.H * a.B >= 1024) qrep *= 2;
+    while (qrep < 8 && ((a.Lq + 128 * 2 * qrep - 1) / (128 * 2 * qrep)) * a.H * a.B >= min_blocks) qrep *= 2;
   const int nq = (a.Lq + 128 * qrep - 1) / (128 * qrep);
   dim3 grid(nq * a.H * a.B), block(256);
   // which kernel runs: resident K/V (cross-attention), two query groups per wave (d = 40 self), the prefetching
