@@ -1,5 +1,7 @@
 #!/bin/bash
 # A/B of the attention kernels: the current library vs a saved baseline (scripts/_ab/libirx_base.so), kbench attn shapes
+# (the baseline: `mkdir -p scripts/_ab && cp image_restoration_and_enhancement_amd/libirx.so scripts/_ab/libirx_base.so`
+#  before the change is built; *.so files are git-ignored)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${1:-ab_attn}; mkdir -p "$O"

@@ -1,6 +1,8 @@
 #!/bin/bash
 # Same-box A/B of the default bench step: the current library vs a saved baseline (scripts/_ab/libirx_base.so),
 # alternated twice; each line -> gpurun_out/<tag>/{new,base}_<i>.json
+# (the baseline: `mkdir -p scripts/_ab && cp image_restoration_and_enhancement_amd/libirx.so scripts/_ab/libirx_base.so`
+#  before the change is built; *.so files are git-ignored)
 set -u
 export IRX_PROF_TOP=${IRX_PROF_TOP:-80}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
