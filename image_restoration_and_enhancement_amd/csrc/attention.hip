@@ -724,8 +724,11 @@ __global__ __launch_bounds__(256, 2) void attn3q_kernel(AttnArgs a) {
 
   // K pad columns: d = 1 (carries -m from Q), d + 1 = the key mask (0; neg_big for keys past Lk, Q[d + 1] = 1), so
   // a ragged last key tile needs no compare / select pass over the scores
-  for (int i = tid; i < 2 * KT * SK; i += 256) Ks2[i] = (i % SK == D) ? one_bits<T>() : (uint16_t)0;
-  for (int i = tid; i < 2 * KT * SV; i += 256) Vs2[i] = (i % SV == D) ? one_bits<T>() : (uint16_t)0;
+  // (16-byte chunks, the pad element selected as a scalar; SK, SV, D multiples of 8)
+  for (int i = tid; i < 2 * KT * SK / 8; i += 256)
+    ((uint4*)Ks2)[i] = make_uint4((8 * i) % SK == D ? (unsigned)one_bits<T>() : 0u, 0u, 0u, 0u);
+  for (int i = tid; i < 2 * KT * SV / 8; i += 256)
+    ((uint4*)Vs2)[i] = make_uint4((8 * i) % SV == D ? (unsigned)one_bits<T>() : 0u, 0u, 0u, 0u);
 
   uint4 kreg[NCH], vreg[NCH];
   const T* kp[NCH];
