@@ -359,8 +359,9 @@ __global__ __launch_bounds__(256, (PF ? PF : attn3_occ<D, KT>())) void attn3_ker
   static_assert(SK % 8 == 0 && SV % 8 == 0, "pad-column chunks");
   // (the pad element selected as a scalar: a select between two uint4 constants becomes a scratch-memory table).
   // d = 160: 164 two-byte stores per thread became 21 (self-attention L = 256 21.6 -> 17.5 us); the streamed d = 80
-  // kernel keeps the element loop (its main loop scheduled 4 % slower with the chunked one, profiles/r06_kbench_attn_init.txt)
-  constexpr bool VINIT = RES || D != 80;
+  // kernel without the prefetch keeps the element loop (its main loop scheduled 4 % slower with the chunked one), its
+  // default PF = 2 form takes the chunks (62 -> 58.5 us, profiles/r06_kbench_attn_init.txt)
+  constexpr bool VINIT = RES || D != 80 || PF != 0;
   if constexpr (VINIT) {
     for (int i = tid; i < 2 * KT * SK / 8; i += 256)
       ((uint4*)Ks2)[i] = make_uint4((DQ > D && (8 * i) % SK == D) ? (unsigned)one_bits<T>() : 0u, 0u, 0u, 0u);
